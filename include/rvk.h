@@ -1,0 +1,116 @@
+/*
+ * rvk.h -- C-ABI of the MI355X RV log-likelihood engine (librvk.so).
+ *
+ * The drop-in boundary for ravest's per-walker log-probability hot path.
+ * Plain pointers and sizes only; no C++ exceptions cross it; every entry point
+ * returns 0 on success or a negative RVK_E* code, and rvk_last_error() gives
+ * the thread's last message.  Non-finite results follow ravest's mask
+ * semantics exactly: an invalid walker yields -INFINITY, never NaN.
+ *
+ * Reference interfaces replaced (ross-dobson/ravest v0.4.0, src/ravest/):
+ *   rvk_create            LogLikelihood.__init__ precompute       fit.py:3535-3598
+ *   rvk_loglike           LogLikelihood.__call__ (batched over W) fit.py:3600-3660
+ *                          incl. Planet(...) conversion/validation model.py:259-275,
+ *                          param.py:88-105,198-234, Planet.radial_velocity
+ *                          model.py:329-354, _compute_rv/_njit_kepler_rv/
+ *                          _solve_kepler model.py:23-243, Trend model.py:483-509
+ *   rvk_loglike_device    same, device-resident in/out, stream-ordered
+ *   rvk_solve_kepler      _solve_kepler                            model.py:23-70
+ *   rvk_predict           Planet/Trend radial_velocity summed per sample
+ *                          (posterior predictive, fit.py:2690-2939)
+ *
+ * theta row layout ("full parameter order"), row-major [W][P_full] fp64:
+ *   for each planet p < n_planets, in parameterisation order:
+ *        [P, K, e | secosw, w | sesinw, Tp | Tc]          (5 values)
+ *   then g[n_inst], jit[n_inst], gd, gdd                  (2*n_inst + 2 values)
+ *   P_full = 5*n_planets + 2*n_inst + 2 (a larger row stride is allowed).
+ * Instrument index i refers to ravest's np.unique (sorted) instrument order
+ * (fit.py:113, 3585-3586).
+ */
+#ifndef RVK_H
+#define RVK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* parameterisation codes (param.py:5-10; ecosw/esinw are disabled upstream) */
+#define RVK_PAR_PKEWTP            0   /* "P K e w Tp" */
+#define RVK_PAR_PKEWTC            1   /* "P K e w Tc" */
+#define RVK_PAR_PKSECOSWSESINWTP  2   /* "P K secosw sesinw Tp" */
+#define RVK_PAR_PKSECOSWSESINWTC  3   /* "P K secosw sesinw Tc" */
+
+#define RVK_MAX_PLANETS 8
+#define RVK_MAX_INST    16
+
+/* error codes */
+#define RVK_OK          0
+#define RVK_E_ARG      -1   /* bad argument / shape */
+#define RVK_E_HIP      -2   /* HIP runtime error */
+#define RVK_E_NODEV    -3   /* no usable gfx950 device */
+#define RVK_E_NOMEM    -4
+
+/* rvk_predict component mask */
+#define RVK_PRED_PLANETS  0x00FFu  /* bit p: include planet p */
+#define RVK_PRED_TREND    0x0100u  /* include gd*(t-t0) + gdd*(t-t0)^2 */
+#define RVK_PRED_GAMMA    0x0200u  /* include g[inst] (needs inst per time) */
+
+typedef struct rvk_handle rvk_handle;
+
+/* Create a handle bound to HIP device `device` (ordinal; -1 = current device).
+ * Copies the data arrays to the device once (LogLikelihood precompute).
+ * inst_idx may be NULL when n_inst == 1. Returns NULL on error. */
+rvk_handle *rvk_create(const double *time, const double *vel, const double *velerr,
+                       const int32_t *inst_idx, int32_t n_epochs, int32_t n_inst,
+                       int32_t n_planets, int32_t parameterisation, double t0,
+                       int32_t device);
+
+void rvk_destroy(rvk_handle *h);
+
+/* Blocking, host buffers: out[w] = log-likelihood of walker w (−inf if a planet
+ * is invalid, exactly where ravest's Planet() raises ValueError). */
+int rvk_loglike(rvk_handle *h, const double *theta, int64_t n_walkers, int64_t row_stride,
+                double *out);
+
+/* Asynchronous, device buffers, stream-ordered on `stream` (a hipStream_t on
+ * the handle's device, used as given: NULL is HIP's default stream; see
+ * rvk_stream() for the handle's own).  Inputs must be resident on that device. */
+int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t n_walkers,
+                       int64_t row_stride, double *d_out, void *stream);
+
+/* Pre-size the handle's device workspace for up to max_walkers per call, so
+ * that rvk_loglike_device never allocates (required before capturing it in a
+ * HIP graph).  Only the Tc / secosw parameterisations use a workspace. */
+int rvk_reserve(rvk_handle *h, int64_t max_walkers);
+
+/* Posterior predictive: out[s][j] = sum of the selected components for sample
+ * s (theta row s) at time t[j]; inst (len n_t) only needed with RVK_PRED_GAMMA.
+ * Invalid planets give NaN rows. Host buffers, blocking. */
+int rvk_predict(rvk_handle *h, const double *theta, int64_t n_samples, int64_t row_stride,
+                const double *t, const int32_t *inst, int64_t n_t, uint32_t what, double *out);
+
+/* Kepler solve on the device for arrays (host buffers): cos E, sin E of
+ * E - e sin E = M.  solver 0: production solver (fp32 seed + fp64 Halley
+ * polish, converged to ~1 ulp); solver 1: ravest's Halley iteration restated
+ * (E0 = M, |dE| < 1.48e-8, <= 50 iterations) in a 2*pi-reduced frame. */
+int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, double *sinE,
+                     int32_t device, int32_t solver);
+
+/* Options. RVK_OPT_SOLVER: 0 = production solver (default), 1 = reference Halley. */
+#define RVK_OPT_SOLVER 1
+int rvk_set_option(rvk_handle *h, int32_t key, int32_t value);
+
+/* Stream the handle uses (hipStream_t as void*). */
+void *rvk_stream(rvk_handle *h);
+int rvk_sync(rvk_handle *h);
+
+int rvk_device_count(void);
+const char *rvk_last_error(void);
+int rvk_version(void);   /* 100*major + minor */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RVK_H */

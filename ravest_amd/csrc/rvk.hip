@@ -1,0 +1,619 @@
+// rvk.hip -- MI355X (gfx950) kernels and the C-ABI of include/rvk.h.
+//
+// Hot path: ravest's LogLikelihood.__call__ (src/ravest/fit.py:3600-3660)
+// batched over walkers.  Mapping (see DESIGN.md "Kernels"):
+//   * one wave64 per walker (grid-stride over walkers); the walker index is
+//     wave-uniform (readfirstlane), so its theta row is fetched with scalar
+//     loads and the per-planet prologue (conversion + validity, param.py) is
+//     computed once per wave;
+//   * lanes stride the epochs: lane l handles epochs l, l+64, ... -- the
+//     time / velocity / velerr^2 / instrument arrays are read coalesced;
+//   * per (walker, epoch): sum over planets of the Kepler RV (Halley in a
+//     2*pi-reduced frame), + trend + gamma[inst]; s^2 = velerr^2 + jit[inst]^2;
+//     chi^2 accumulates in a register and sum(log s^2) as a renormalised
+//     running product (frexp), so the epoch loop has no log;
+//   * a wave64 butterfly reduction gives 1 fp64 per walker; -inf for
+//     invalid walkers (mask semantics of fit.py:3622-3627).
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rvk.h"
+#include "rvk_math.h"
+
+using namespace rvk;
+
+namespace {
+
+constexpr int kBlock = 256;          // 4 waves
+#ifndef RVK_LB_WAVES
+#define RVK_LB_WAVES 1                // __launch_bounds__ min waves per SIMD for loglike_kernel
+#endif
+constexpr int kWavesPerBlock = kBlock / 64;
+
+// Per-epoch data: SoA, device-resident for the handle's lifetime.
+struct EpochData {
+    const double *t;      // time
+    const double *vel;
+    const double *s2;     // velerr^2 (fit.py:3598)
+    const int32_t *inst;  // instrument index (fit.py:3586)
+    const SC *tab;        // sin/cos table (rvk_math.h, kTabN entries)
+    double t0;            // Trend reference time (model.py:486,491)
+};
+
+// Copy the sin/cos table into LDS (whole block; one barrier, before any
+// per-wave work so no wave can skip it).
+__device__ __forceinline__ void load_tab(SC *lds, const SC *__restrict__ g) {
+    for (int i = threadIdx.x; i < kTabN; i += blockDim.x) lds[i] = g[i];
+    __syncthreads();
+}
+
+// Block-level structure.  A block (4 waves) owns passes of up to WB walkers
+// (contiguous).  Each pass:
+//   1. prep, lane-parallel over (walker, planet): thread k builds PlanetK for
+//      walker k/NP, planet k%NP into LDS -- one conversion latency per pass
+//      instead of one per walker, and no planet state lives in registers;
+//        FUSED = true : "P K e w Tp" computed here (IEEE div, sqrt, sincos; no
+//                       OCML atan/tan, so the kernel keeps its register budget);
+//        FUSED = false: copied from the prep kernel's workspace (Tc and
+//                       secosw/sesinw need atan/tan/atan2);
+//   2. __syncthreads (the first pass also covers the sin/cos table fill);
+//   3. wave wv evaluates walkers wv, wv+4, ... of the pass: lanes stride the
+//      epochs, planet constants are re-read from LDS with a wave-uniform
+//      address (broadcast), a wave64 butterfly gives the walker's sum.
+template <int NP>
+struct PassCfg {
+    static constexpr int WB = (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
+};
+
+template <int NP, bool MULTI, int SOLVER, bool FUSED>
+__global__ __launch_bounds__(kBlock, RVK_LB_WAVES) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
+                                                         const double *__restrict__ theta, long long n_walkers,
+                                                         long long stride, int wb, const PlanetK *__restrict__ ws,
+                                                         const int *__restrict__ ws_ok, double *__restrict__ out) {
+    constexpr int WB = PassCfg<NP>::WB;
+    __shared__ PlanetK pks[WB][NP];
+    __shared__ int okw[WB];
+    __shared__ SC tab[kTabN];
+    for (int i = threadIdx.x; i < kTabN; i += kBlock) tab[i] = d.tab[i];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
+        const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
+        if (threadIdx.x < WB) okw[threadIdx.x] = 1;
+        __syncthreads();
+        for (int k = threadIdx.x; k < nb * NP; k += kBlock) {
+            const int j = k / NP, p = k - j * NP;
+            const long long w = base + j;
+            PlanetK pk;
+            bool ok;
+            if (FUSED) {
+                ok = planet_consts_t<0>(theta + w * stride + 5 * p, pk);
+            } else {
+                pk = ws[w * NP + p];
+                ok = ws_ok[w * NP + p] != 0;
+            }
+            pks[j][p] = pk;
+            if (!ok) okw[j] = 0;
+        }
+        __syncthreads();
+        for (int j = wv; j < nb; j += kWavesPerBlock) {
+            const long long w = base + j;
+            const double *row = theta + w * stride;
+            if (!okw[j]) {
+                if (lane == 0) out[w] = -INFINITY;
+                continue;
+            }
+            const double *g = row + 5 * NP;
+            const double *jit = g + n_inst;
+            const double gd = jit[n_inst], gdd = jit[n_inst + 1];
+            const double g0 = g[0], j0 = jit[0] * jit[0];
+            double chi2 = 0.0, prod = 1.0;
+            int expo = 0;
+            // software pipeline: the next epoch's data is in flight during this epoch's solve
+            int i = lane;
+            double tn = 0.0, vn = 0.0, sn = 1.0;
+            int in_ = 0;
+            if (i < n_epochs) {
+                tn = d.t[i]; vn = d.vel[i]; sn = d.s2[i];
+                if (MULTI) in_ = d.inst[i];
+            }
+            for (; i < n_epochs; i += 64) {
+                const double t = tn, vel = vn, s2b = sn;
+                const int ii = in_;
+                const int inx = i + 64;
+                if (inx < n_epochs) {
+                    tn = d.t[inx]; vn = d.vel[inx]; sn = d.s2[inx];
+                    if (MULTI) in_ = d.inst[inx];
+                }
+                double rv = 0.0;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) rv += planet_rv<SOLVER>(pks[j][p], t, tab);
+                const double dt = t - d.t0;
+                rv += __builtin_fma(gd, dt, gdd * (dt * dt));
+                double gam = g0, jj = j0;
+                if (MULTI) {
+                    for (int k = 1; k < n_inst; ++k) {
+                        if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
+                    }
+                }
+                rv += gam;
+                const double s2 = s2b + jj;
+                const double r = rv - vel;
+                chi2 = __builtin_fma(r * r, rcp_nr(s2), chi2);
+                prod *= s2;
+                int ex;
+                prod = __builtin_frexp(prod, &ex);
+                expo += ex;
+            }
+            double lsum = log(prod) + (double)expo * kLn2;
+            double tot = wave_sum(chi2 + lsum);
+            if (lane == 0) out[w] = -0.5 * (tot + (double)n_epochs * kLog2Pi);
+        }
+        __syncthreads();   // pks/okw are rewritten by the next pass
+    }
+}
+
+// Per-(walker, planet) conversion for the Tc / secosw parameterisations
+// (param.py:198-234, 299-362), one thread each; feeds loglike_kernel<..., false>.
+__global__ __launch_bounds__(256) void prep_kernel(int par, int np, const double *__restrict__ theta,
+                                                   long long n_walkers, long long stride, PlanetK *__restrict__ ws,
+                                                   int *__restrict__ ws_ok) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n_walkers * np) return;
+    long long w = idx / np;
+    int p = (int)(idx - w * np);
+    PlanetK pk;
+    bool ok = planet_consts(par, theta + w * stride + 5 * p, pk);
+    ws[idx] = pk;
+    ws_ok[idx] = ok ? 1 : 0;
+}
+
+// Posterior predictive (fit.py:2690-2939): one wave per sample, lanes over times.
+template <int NP, int SOLVER>
+__global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restrict__ tq, const int32_t *__restrict__ iq,
+                                                         long long n_t, int n_planets_total, int n_inst, int par,
+                                                         double t0, const double *__restrict__ theta,
+                                                         long long n_samples, long long stride, unsigned what,
+                                                         const SC *__restrict__ gtab, double *__restrict__ out) {
+    __shared__ SC tab[kTabN];
+    load_tab(tab, gtab);
+    const int lane = threadIdx.x & 63;
+    const long long wave0 = (long long)blockIdx.x * kWavesPerBlock +
+                            __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
+    for (long long s = wave0; s < n_samples; s += nwaves) {
+        const double *row = theta + s * stride;
+        PlanetK pk[NP > 0 ? NP : 1];
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {   // q-th selected planet = q-th set bit of `what`
+            unsigned m = what & RVK_PRED_PLANETS;
+            for (int k = 0; k < q; ++k) m &= m - 1u;
+            ok &= planet_consts(par, row + 5 * __builtin_ctz(m), pk[q]);
+        }
+        const double *g = row + 5 * n_planets_total;
+        const double *jit = g + n_inst;
+        const double gd = jit[n_inst], gdd = jit[n_inst + 1];
+        for (long long j = lane; j < n_t; j += 64) {
+            double v = 0.0;
+            const double t = tq[j];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) v += planet_rv<SOLVER>(pk[p], t, tab);
+            if (what & RVK_PRED_TREND) {
+                const double dt = t - t0;
+                v += __builtin_fma(gd, dt, gdd * (dt * dt));
+            }
+            if (what & RVK_PRED_GAMMA) v += g[iq ? iq[j] : 0];
+            out[s * n_t + j] = ok ? v : NAN;
+        }
+    }
+}
+
+template <int SOLVER>
+__global__ __launch_bounds__(256) void kepler_kernel(const double *__restrict__ M, const double *__restrict__ e,
+                                                     long long n, const SC *__restrict__ gtab,
+                                                     double *__restrict__ cosE, double *__restrict__ sinE) {
+    __shared__ SC tab[kTabN];
+    load_tab(tab, gtab);
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        double c, s;
+        const double ee = e[i];
+        if (SOLVER == 1) solve_kepler_ref(M[i], ee, c, s);
+        else solve_kepler_fast(M[i], ee, 6.0 * ee * ee * ee, tab, c, s);
+        cosE[i] = c;
+        sinE[i] = s;
+    }
+}
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(RVK_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
+    } while (0)
+
+typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long,
+                                 const PlanetK *, const int *, double *);
+
+// Grid: one pass per block when W is small (4 walkers per block = 1 per wave);
+// for large W at most kMaxBlocks blocks, each looping over passes of <= WB walkers.
+constexpr long long kMaxBlocks = 2048;
+
+template <int NP, bool MULTI, int SOLVER, bool FUSED>
+void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
+               const PlanetK *ws, const int *ws_ok, double *out) {
+    constexpr int WB = PassCfg<NP>::WB;
+    long long blocks = (W + kWavesPerBlock - 1) / kWavesPerBlock;
+    int wb = kWavesPerBlock;
+    if (blocks > kMaxBlocks) {
+        long long per = (W + kMaxBlocks - 1) / kMaxBlocks;                 // walkers per block
+        per = ((per + kWavesPerBlock - 1) / kWavesPerBlock) * kWavesPerBlock;
+        wb = (int)(per < WB ? per : WB);
+        blocks = (W + wb - 1) / wb;
+        if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+    }
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, FUSED>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
+                       ni, th, W, stride, wb, ws, ws_ok, out);
+}
+
+template <bool MULTI, int SOLVER, bool FUSED>
+loglike_launch_t pick_ll_s(int np) {
+    switch (np) {
+        case 1: return launch_ll<1, MULTI, SOLVER, FUSED>;
+        case 2: return launch_ll<2, MULTI, SOLVER, FUSED>;
+        case 3: return launch_ll<3, MULTI, SOLVER, FUSED>;
+        case 4: return launch_ll<4, MULTI, SOLVER, FUSED>;
+        case 5: return launch_ll<5, MULTI, SOLVER, FUSED>;
+        case 6: return launch_ll<6, MULTI, SOLVER, FUSED>;
+        case 7: return launch_ll<7, MULTI, SOLVER, FUSED>;
+        case 8: return launch_ll<8, MULTI, SOLVER, FUSED>;
+        default: return nullptr;
+    }
+}
+
+template <int SOLVER, bool FUSED>
+loglike_launch_t pick_ll_f(int np, bool multi) {
+    return multi ? pick_ll_s<true, SOLVER, FUSED>(np) : pick_ll_s<false, SOLVER, FUSED>(np);
+}
+
+loglike_launch_t pick_ll(int np, bool multi, int solver, bool fused) {
+    if (solver == 1) return fused ? pick_ll_f<1, true>(np, multi) : pick_ll_f<1, false>(np, multi);
+    return fused ? pick_ll_f<0, true>(np, multi) : pick_ll_f<0, false>(np, multi);
+}
+
+int check_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RVK_E_NODEV, std::string("device is ") + prop.gcnArchName + ", librvk is built for gfx950 only");
+    return RVK_OK;
+}
+
+std::vector<SC> host_table() {
+    std::vector<SC> t(kTabN);
+    for (int j = -kTabHalf; j <= kTabHalf; ++j) {
+        const double a = (double)j * kTabH;   // identical rounding to the device's jj * kTabH
+        t[j + kTabHalf] = SC{std::sin(a), std::cos(a)};
+    }
+    return t;
+}
+
+int upload_table(SC **d_tab) {
+    std::vector<SC> t = host_table();
+    HIPCHK(hipMalloc(d_tab, sizeof(SC) * kTabN));
+    HIPCHK(hipMemcpy(*d_tab, t.data(), sizeof(SC) * kTabN, hipMemcpyHostToDevice));
+    return RVK_OK;
+}
+
+dim3 wave_grid(long long items) {
+    long long blocks = (items + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > (1LL << 20)) blocks = 1LL << 20;
+    if (blocks < 1) blocks = 1;
+    return dim3((unsigned)blocks);
+}
+
+}  // namespace
+
+struct rvk_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n = 0, n_inst = 1, n_planets = 1, par = 0;
+    double t0 = 0.0;
+    double *d_t = nullptr, *d_vel = nullptr, *d_s2 = nullptr;
+    SC *d_tab = nullptr;
+    int32_t *d_inst = nullptr;
+    // scratch for the host-buffer entry points
+    double *d_theta = nullptr, *d_out = nullptr;
+    size_t cap_theta = 0, cap_out = 0;
+    // prep-kernel workspace (parameterisations other than "P K e w Tp")
+    PlanetK *d_ws = nullptr;
+    int *d_ws_ok = nullptr;
+    long long cap_ws = 0;   // walkers
+    loglike_launch_t launch = nullptr;
+    int solver = 0;
+};
+
+extern "C" {
+
+int rvk_version(void) { return 100; }
+
+const char *rvk_last_error(void) { return g_err.c_str(); }
+
+int rvk_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int grow(double **p, size_t *cap, size_t need) {
+    if (need <= *cap) return RVK_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need));
+    *cap = need;
+    return RVK_OK;
+}
+
+static void free_handle(rvk_handle *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipFree(h->d_t);
+    (void)hipFree(h->d_tab);
+    (void)hipFree(h->d_vel);
+    (void)hipFree(h->d_s2);
+    (void)hipFree(h->d_inst);
+    (void)hipFree(h->d_theta);
+    (void)hipFree(h->d_out);
+    (void)hipFree(h->d_ws);
+    (void)hipFree(h->d_ws_ok);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+static int create_impl(rvk_handle *h, const double *time, const double *vel, const double *velerr,
+                       const int32_t *inst_idx, int32_t n, int32_t n_inst, int32_t n_planets, int32_t par,
+                       double t0, int32_t device) {
+    if (n < 1 || !time || !vel || !velerr) return fail(RVK_E_ARG, "n_epochs must be >= 1 with non-NULL data");
+    if (n_planets < 1 || n_planets > RVK_MAX_PLANETS) return fail(RVK_E_ARG, "n_planets must be in [1, 8]");
+    if (n_inst < 1 || n_inst > RVK_MAX_INST) return fail(RVK_E_ARG, "n_inst must be in [1, 16]");
+    if (par < 0 || par > 3) return fail(RVK_E_ARG, "unknown parameterisation code");
+    if (n_inst > 1 && !inst_idx) return fail(RVK_E_ARG, "inst_idx is required when n_inst > 1");
+    std::vector<int32_t> inst(n, 0);
+    if (inst_idx)
+        for (int i = 0; i < n; ++i) {
+            if (inst_idx[i] < 0 || inst_idx[i] >= n_inst) return fail(RVK_E_ARG, "inst_idx out of range");
+            inst[i] = inst_idx[i];
+        }
+    int ndev = rvk_device_count();
+    if (ndev < 1) return fail(RVK_E_NODEV, "no HIP device visible");
+    if (device < 0) HIPCHK(hipGetDevice(&device));
+    if (device >= ndev) return fail(RVK_E_ARG, "device ordinal out of range");
+    int rc = check_gfx950(device);
+    if (rc) return rc;
+    h->device = device;
+    h->n = n;
+    h->n_inst = n_inst;
+    h->n_planets = n_planets;
+    h->par = par;
+    h->t0 = t0;
+    h->launch = pick_ll(n_planets, n_inst > 1, 0, par == RVK_PAR_PKEWTP);
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    std::vector<double> s2(n);
+    for (int i = 0; i < n; ++i) s2[i] = velerr[i] * velerr[i];     // velerr ** 2 (fit.py:3598)
+    size_t bd = sizeof(double) * (size_t)n;
+    HIPCHK(hipMalloc(&h->d_t, bd));
+    HIPCHK(hipMalloc(&h->d_vel, bd));
+    HIPCHK(hipMalloc(&h->d_s2, bd));
+    HIPCHK(hipMalloc(&h->d_inst, sizeof(int32_t) * (size_t)n));
+    HIPCHK(hipMemcpy(h->d_t, time, bd, hipMemcpyHostToDevice));
+    if ((rc = upload_table(&h->d_tab))) return rc;
+    HIPCHK(hipMemcpy(h->d_vel, vel, bd, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_s2, s2.data(), bd, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_inst, inst.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice));
+    return RVK_OK;
+}
+
+rvk_handle *rvk_create(const double *time, const double *vel, const double *velerr, const int32_t *inst_idx,
+                       int32_t n_epochs, int32_t n_inst, int32_t n_planets, int32_t parameterisation, double t0,
+                       int32_t device) {
+    rvk_handle *h = new (std::nothrow) rvk_handle();
+    if (!h) {
+        fail(RVK_E_NOMEM, "out of host memory");
+        return nullptr;
+    }
+    if (create_impl(h, time, vel, velerr, inst_idx, n_epochs, n_inst, n_planets, parameterisation, t0, device)) {
+        free_handle(h);
+        return nullptr;
+    }
+    return h;
+}
+
+void rvk_destroy(rvk_handle *h) { free_handle(h); }
+
+void *rvk_stream(rvk_handle *h) { return h ? (void *)h->stream : nullptr; }
+
+int rvk_set_option(rvk_handle *h, int32_t key, int32_t value) {
+    if (!h) return fail(RVK_E_ARG, "NULL handle");
+    if (key == RVK_OPT_SOLVER) {
+        if (value != 0 && value != 1) return fail(RVK_E_ARG, "solver must be 0 (fast) or 1 (reference Halley)");
+        h->solver = value;
+        h->launch = pick_ll(h->n_planets, h->n_inst > 1, value, h->par == RVK_PAR_PKEWTP);
+        return RVK_OK;
+    }
+    return fail(RVK_E_ARG, "unknown option key");
+}
+
+int rvk_sync(rvk_handle *h) {
+    if (!h) return fail(RVK_E_ARG, "NULL handle");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RVK_OK;
+}
+
+static int check_rows(rvk_handle *h, int64_t W, int64_t stride) {
+    if (!h) return fail(RVK_E_ARG, "NULL handle");
+    if (W < 0) return fail(RVK_E_ARG, "n_walkers < 0");
+    long long pfull = 5LL * h->n_planets + 2LL * h->n_inst + 2;
+    if (stride < pfull) return fail(RVK_E_ARG, "row_stride < P_full = 5*n_planets + 2*n_inst + 2");
+    return RVK_OK;
+}
+
+static int reserve_ws(rvk_handle *h, long long W) {
+    if (h->par == RVK_PAR_PKEWTP || W <= h->cap_ws) return RVK_OK;
+    (void)hipFree(h->d_ws);
+    (void)hipFree(h->d_ws_ok);
+    h->d_ws = nullptr;
+    h->d_ws_ok = nullptr;
+    h->cap_ws = 0;
+    HIPCHK(hipMalloc(&h->d_ws, sizeof(PlanetK) * (size_t)W * h->n_planets));
+    HIPCHK(hipMalloc(&h->d_ws_ok, sizeof(int) * (size_t)W * h->n_planets));
+    h->cap_ws = W;
+    return RVK_OK;
+}
+
+int rvk_reserve(rvk_handle *h, int64_t max_walkers) {
+    if (!h || max_walkers < 0) return fail(RVK_E_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    return reserve_ws(h, max_walkers);
+}
+
+int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t W, int64_t stride, double *d_out,
+                       void *stream) {
+    int rc = check_rows(h, W, stride);
+    if (rc) return rc;
+    if (W == 0) return RVK_OK;
+    if (!d_theta || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
+    hipStream_t st = (hipStream_t)stream;   // used as given: NULL is HIP's default stream
+    HIPCHK(hipSetDevice(h->device));
+    if ((rc = reserve_ws(h, W))) return rc;
+    if (h->par != RVK_PAR_PKEWTP) {
+        long long items = W * (long long)h->n_planets;
+        hipLaunchKernelGGL(prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, h->par,
+                           h->n_planets, d_theta, (long long)W, (long long)stride, h->d_ws, h->d_ws_ok);
+    }
+    EpochData d{h->d_t, h->d_vel, h->d_s2, h->d_inst, h->d_tab, h->t0};
+    h->launch(st, d, h->n, h->n_inst, d_theta, W, stride, h->d_ws, h->d_ws_ok, d_out);
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_loglike(rvk_handle *h, const double *theta, int64_t W, int64_t stride, double *out) {
+    int rc = check_rows(h, W, stride);
+    if (rc) return rc;
+    if (W == 0) return RVK_OK;
+    if (!theta || !out) return fail(RVK_E_ARG, "NULL host buffer");
+    HIPCHK(hipSetDevice(h->device));
+    size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
+    if ((rc = grow(&h->d_theta, &h->cap_theta, bt))) return rc;
+    if ((rc = grow(&h->d_out, &h->cap_out, bo))) return rc;
+    HIPCHK(hipMemcpyAsync(h->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_loglike_device(h, h->d_theta, W, stride, h->d_out, h->stream))) return rc;
+    HIPCHK(hipMemcpyAsync(out, h->d_out, bo, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RVK_OK;
+}
+
+int rvk_predict(rvk_handle *h, const double *theta, int64_t S, int64_t stride, const double *t,
+                const int32_t *inst, int64_t n_t, uint32_t what, double *out) {
+    int rc = check_rows(h, S, stride);
+    if (rc) return rc;
+    if (S == 0 || n_t == 0) return RVK_OK;
+    if (!theta || !t || !out) return fail(RVK_E_ARG, "NULL host buffer");
+    if ((what & RVK_PRED_GAMMA) && h->n_inst > 1 && !inst) return fail(RVK_E_ARG, "inst required for GAMMA");
+    unsigned planets = what & RVK_PRED_PLANETS & ((1u << h->n_planets) - 1u);
+    int nsel = __builtin_popcount(planets);
+    what = (what & ~RVK_PRED_PLANETS) | planets;
+    HIPCHK(hipSetDevice(h->device));
+    double *d_th = nullptr, *d_t = nullptr, *d_o = nullptr;
+    int32_t *d_i = nullptr;
+    size_t bt = sizeof(double) * (size_t)S * (size_t)stride;
+    HIPCHK(hipMalloc(&d_th, bt));
+    HIPCHK(hipMalloc(&d_t, sizeof(double) * n_t));
+    HIPCHK(hipMalloc(&d_o, sizeof(double) * S * n_t));
+    if (inst) {
+        HIPCHK(hipMalloc(&d_i, sizeof(int32_t) * n_t));
+        HIPCHK(hipMemcpyAsync(d_i, inst, sizeof(int32_t) * n_t, hipMemcpyHostToDevice, h->stream));
+    }
+    HIPCHK(hipMemcpyAsync(d_th, theta, bt, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(d_t, t, sizeof(double) * n_t, hipMemcpyHostToDevice, h->stream));
+    dim3 grid = wave_grid(S);
+#define PRED_CASE(K)                                                                                        \
+    case K:                                                                                                 \
+        if (h->solver == 1)                                                                                 \
+            hipLaunchKernelGGL((predict_kernel<K, 1>), grid, dim3(kBlock), 0, h->stream, d_t, d_i,           \
+                               (long long)n_t, h->n_planets, h->n_inst, h->par, h->t0, d_th, (long long)S,  \
+                               (long long)stride, what, h->d_tab, d_o);                                     \
+        else                                                                                                \
+            hipLaunchKernelGGL((predict_kernel<K, 0>), grid, dim3(kBlock), 0, h->stream, d_t, d_i,           \
+                               (long long)n_t, h->n_planets, h->n_inst, h->par, h->t0, d_th, (long long)S,  \
+                               (long long)stride, what, h->d_tab, d_o);                                     \
+        break;
+    switch (nsel) {
+        PRED_CASE(0) PRED_CASE(1) PRED_CASE(2) PRED_CASE(3) PRED_CASE(4) PRED_CASE(5) PRED_CASE(6)
+        PRED_CASE(7) PRED_CASE(8)
+    }
+#undef PRED_CASE
+    hipError_t le = hipGetLastError();
+    HIPCHK(hipMemcpyAsync(out, d_o, sizeof(double) * S * n_t, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    (void)hipFree(d_th);
+    (void)hipFree(d_t);
+    (void)hipFree(d_o);
+    (void)hipFree(d_i);
+    if (le != hipSuccess) return fail(RVK_E_HIP, std::string("predict_kernel: ") + hipGetErrorString(le));
+    return RVK_OK;
+}
+
+int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, double *sinE, int32_t device,
+                     int32_t solver) {
+    if (n < 0 || (n > 0 && (!M || !e || !cosE || !sinE))) return fail(RVK_E_ARG, "bad arguments");
+    if (n == 0) return RVK_OK;
+    if (rvk_device_count() < 1) return fail(RVK_E_NODEV, "no HIP device visible");
+    if (device < 0) HIPCHK(hipGetDevice(&device));
+    int rc = check_gfx950(device);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(device));
+    double *dM, *de, *dc, *ds;
+    SC *dtab;
+    if ((rc = upload_table(&dtab))) return rc;
+    size_t b = sizeof(double) * (size_t)n;
+    HIPCHK(hipMalloc(&dM, b));
+    HIPCHK(hipMalloc(&de, b));
+    HIPCHK(hipMalloc(&dc, b));
+    HIPCHK(hipMalloc(&ds, b));
+    HIPCHK(hipMemcpy(dM, M, b, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(de, e, b, hipMemcpyHostToDevice));
+    if (solver == 1)
+        hipLaunchKernelGGL(kepler_kernel<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dM, de, (long long)n,
+                           dtab, dc, ds);
+    else
+        hipLaunchKernelGGL(kepler_kernel<0>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dM, de, (long long)n,
+                           dtab, dc, ds);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(cosE, dc, b, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sinE, ds, b, hipMemcpyDeviceToHost));
+    (void)hipFree(dM);
+    (void)hipFree(de);
+    (void)hipFree(dc);
+    (void)hipFree(ds);
+    (void)hipFree(dtab);
+    return RVK_OK;
+}
+
+}  // extern "C"

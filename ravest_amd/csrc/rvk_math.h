@@ -1,0 +1,306 @@
+// rvk_math.h -- fp64 device math for the Kepler/RV hot path on gfx950.
+//
+// Everything here is wave64 VALU code: no LDS, no MFMA (the path has no dense
+// contraction).  Two Kepler solvers, both for E - e sin E = M:
+//
+//  * solve_kepler_ref  -- ravest's _solve_kepler (src/ravest/model.py:23-70)
+//    restated: Halley seeded at E0 = M, stop at |E_new - E| < 1.48e-8, at most
+//    50 iterations, result sin/cos(E_new), in a 2*pi-reduced frame.  Halley is
+//    2*pi-equivariant, so iterates and iteration counts are the reference's
+//    shifted by 2*pi*k; only rounding at the |M|*eps level differs (the
+//    reference carries that rounding in E itself).  Selected with
+//    RVK_OPT_SOLVER = 1.
+//
+//  * solve_kepler_fast -- the production solver (default).  It converges to
+//    the same root to ~1 ulp, so cos E / sin E match the reference's converged
+//    values within the stated fp64 tolerance:
+//      1. r = M reduced to [-pi, pi] (Cody-Waite, FMA);
+//      2. fp32 Halley seed from E0 = r with the hardware v_sin_f32/v_cos_f32
+//         (accurate fp32 polynomials when e > 0.95, wave-uniform branch);
+//         per-lane exit at |dE| < 2e-5, at most 8 iterations -- the large early
+//         steps cost fp32 issue slots, not fp64 ones;
+//      3. sin/cos of the fp32 root in fp64 from an LDS table of sin/cos at
+//         j*pi/128 plus a degree-7/8 Taylor rotation (|d| <= pi/256);
+//      4. Householder order-3 steps (quartic convergence) with sin/cos carried
+//         by short-series rotation, until the local error estimate
+//         (e/f')^3 d^4 < 1e-17: one step for a seed within ~1e-4 unless e is
+//         close to 1.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rvk {
+
+constexpr double kPi      = 3.141592653589793;        // == np.pi
+constexpr double kTwoPi   = 6.283185307179586;        // == 2*np.pi (exact doubling)
+constexpr double kInv2Pi  = 0.15915494309189535;
+constexpr double k2PiHi   = 6.283185307179586232e+00; // 0x401921FB54442D18
+constexpr double k2PiMi   = 2.449293598294706414e-16; // 0x3CB1A62633145C07
+constexpr double k2PiLo   = -5.989539619436679332e-33;
+constexpr double k2OverPi = 0.6366197723675814;
+constexpr double kPio2Hi  = 1.5707963267948966e+00;   // 0x3FF921FB54442D18
+constexpr double kPio2Mi  = 6.123233995736766e-17;    // 0x3C91A62633145C07
+constexpr double kPio2Lo  = -1.4973849048591698e-33;
+constexpr double kLn2     = 0.6931471805599453;
+constexpr double kLog2Pi  = 1.8378770664093453;       // == np.log(2*np.pi)
+
+// Reduce x by 2*pi: r = x - k*2*pi, |r| <= pi (+ulp), abs error ~1e-15 for any |x| < 1e15.
+__device__ __forceinline__ double reduce_2pi(double x) {
+    double k = __builtin_rint(x * kInv2Pi);
+    double r = __builtin_fma(-k, k2PiHi, x);
+    r = __builtin_fma(-k, k2PiMi, r);
+    return __builtin_fma(-k, k2PiLo, r);
+}
+
+// sin and cos of a moderate argument (|x| < ~1e5) in one pass: quadrant
+// reduction by pi/2 (3-part Cody-Waite with FMA) and the classic fdlibm
+// minimax kernels (__kernel_sin / __kernel_cos coefficients, < 1 ulp on
+// [-pi/4, pi/4]).  Branch-free: the quadrant is applied with selects.
+__device__ __forceinline__ void sincos_mod(double x, double &s, double &c) {
+    constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                     S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                     S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                     C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                     C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double k = __builtin_rint(x * k2OverPi);
+    double y = __builtin_fma(-k, kPio2Hi, x);
+    y = __builtin_fma(-k, kPio2Mi, y);
+    y = __builtin_fma(-k, kPio2Lo, y);
+    int q = (int)k;
+    double z = y * y;
+    double rs = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, S6, S5), S4), S3), S2);
+    double sn = __builtin_fma(z * y, __builtin_fma(z, rs, S1), y);
+    double rc = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, C6, C5), C4), C3), C2), C1);
+    double hz = 0.5 * z;
+    double w = 1.0 - hz;
+    double cs = w + (((1.0 - w) - hz) + z * rc);
+    double ss = (q & 1) ? cs : sn;
+    double cc = (q & 1) ? sn : cs;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+}
+
+// fp32 sin/cos for the seed stage, |x| <~ 10: quadrant reduction + short
+// minimax polynomials (abs error ~1e-7, relative near 0).
+__device__ __forceinline__ void sincos_f32(float x, float &s, float &c) {
+    float k = __builtin_rintf(x * 0.636619772f);
+    float y = __builtin_fmaf(-k, 1.57079637f, x);
+    y = __builtin_fmaf(-k, -4.37113883e-8f, y);
+    int q = (int)k;
+    float z = y * y;
+    float sn = __builtin_fmaf(z * y, __builtin_fmaf(z, __builtin_fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f),
+                                                    -1.6666654611e-1f), y);
+    float cs = __builtin_fmaf(z, __builtin_fmaf(z, __builtin_fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f),
+                                                4.166664568298827e-2f), -0.5f);
+    cs = __builtin_fmaf(z, cs, 1.0f);
+    float ss = (q & 1) ? cs : sn;
+    float cc = (q & 1) ? sn : cs;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+}
+
+// 1/b to ~1 ulp: v_rcp_f64 + two Newton-Raphson steps (finite, normal b).
+__device__ __forceinline__ double rcp_nr(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double t = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, t, r);
+    t = __builtin_fma(-b, r, 1.0);
+    return __builtin_fma(r, t, r);
+}
+
+// ---- reference-faithful solver (RVK_OPT_SOLVER = 1) ---------------------------------
+__device__ __forceinline__ void solve_kepler_ref(double M, double e, double &cosE, double &sinE) {
+    const double tol = 1.48e-08;
+    const double r = reduce_2pi(M);
+    double E = r, s = 0.0, c = 0.0;
+    bool done = false;
+#pragma unroll 1
+    for (int it = 0; it < 50; ++it) {
+        sincos_mod(E, s, c);
+        double f = E - e * s - r;
+        double fp = 1.0 - e * c;
+        double fpp = e * s;
+        double En = E - f / (fp - (f * fpp) / (2.0 * fp));
+        bool conv = __builtin_fabs(En - E) < tol;
+        E = En;
+        if (conv) { done = true; break; }
+    }
+    if (done) sincos_mod(E, s, c);   // sin/cos(E_new); else last iterate's (maxiter semantics)
+    cosE = c;
+    sinE = s;
+}
+
+// ---- production solver -------------------------------------------------------------
+// sin/cos table for step 3: entries j = -kTabHalf..kTabHalf at a_j = j*kTabH
+// (a_j rounded exactly as the device's jj*kTabH), filled by the host with libm.
+constexpr int kTabHalf = 245;                 // covers |E| <= 6.01
+constexpr int kTabN = 2 * kTabHalf + 1;
+constexpr double kTabH = 0.02454369260617026;  // == np.pi / 128
+constexpr double kTabInvH = 40.74366543152521; // == 128 / np.pi
+
+struct SC { double s, c; };
+
+__device__ __forceinline__ void sincos_tab(double E, const SC *tab, double &S, double &C) {
+    double jj = __builtin_rint(E * kTabInvH);
+    jj = __builtin_fmin(__builtin_fmax(jj, (double)-kTabHalf), (double)kTabHalf);
+    const double a = jj * kTabH;                 // same rounding as the host's j*h
+    const double d = E - a;                      // exact (Sterbenz)
+    const SC sc = tab[(int)jj + kTabHalf];
+    const double z = d * d;
+    const double sd = __builtin_fma(d * z, __builtin_fma(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
+    const double cm = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
+    S = __builtin_fma(sc.s, cm, __builtin_fma(sc.c, sd, sc.s));
+    C = __builtin_fma(sc.c, cm, __builtin_fma(-sc.s, sd, sc.c));
+}
+
+template <bool PRECISE32>
+__device__ __forceinline__ float seed_f32(float rf, float ef) {
+    float Ef = rf;
+#pragma unroll 1
+    for (int it = 0; it < 8; ++it) {
+        float s, c;
+        if (PRECISE32) {
+            sincos_f32(Ef, s, c);
+        } else {
+            const float x = Ef * 0.159154943f;   // v_sin/v_cos take revolutions
+            s = __builtin_amdgcn_sinf(x);
+            c = __builtin_amdgcn_cosf(x);
+        }
+        const float f = Ef - ef * s - rf;
+        const float fp = 1.0f - ef * c;
+        const float fpp = ef * s;
+        const float den = __builtin_fmaf(-0.5f * f, fpp, fp * fp);
+        const float d = f * fp * __builtin_amdgcn_rcpf(den);
+        Ef -= d;
+        if (__builtin_fabsf(d) < 2e-5f) break;
+    }
+    return Ef;
+}
+
+// e6e3 = 6*e^3 (per planet, precomputed).
+__device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e3, const SC *tab, double &cosE,
+                                                  double &sinE) {
+    const double r = reduce_2pi(M);
+    const float rf = (float)r, ef = (float)e;
+#ifndef RVK_SEED_HW
+#define RVK_SEED_HW 1
+#endif
+    const float Ef = (!RVK_SEED_HW || ef > 0.95f) ? seed_f32<true>(rf, ef) : seed_f32<false>(rf, ef);
+    double E = (double)Ef, S, C;
+    sincos_tab(E, tab, S, C);
+#pragma unroll 1
+    for (int it = 0; it < 8; ++it) {
+        const double f = E - e * S - r;
+        const double f1 = 1.0 - e * C;
+        const double f2 = e * S;
+        const double f3 = e * C;
+        const double f11 = f1 * f1;
+        const double num = f * __builtin_fma(-3.0 * f, f2, 6.0 * f11);                        // f (6 f1^2 - 3 f f2)
+        const double den = __builtin_fma(f * f, f3, 6.0 * f1 * __builtin_fma(-f, f2, f11));  // 6f1^3 - 6 f f1 f2 + f^2 f3
+        double t = __builtin_amdgcn_rcp(den);
+        t = __builtin_fma(t, __builtin_fma(-den, t, 1.0), t);
+        const double d = -num * t;
+        E += d;
+        const double ad = __builtin_fabs(d);
+        if (ad > 1e-4) {                   // too far for the short series: re-anchor on the table
+            sincos_tab(E, tab, S, C);
+        } else {
+            const double z = d * d;
+            const double sd = __builtin_fma(d * z, -1.0 / 6.0, d);
+            const double cm = z * __builtin_fma(z, 1.0 / 24.0, -0.5);
+            const double Sn = __builtin_fma(S, cm, __builtin_fma(C, sd, S));
+            const double Cn = __builtin_fma(C, cm, __builtin_fma(-S, sd, C));
+            S = Sn;
+            C = Cn;
+        }
+        // next error ~ (e/f1)^3 d^4 ~ 6 e^3 d^4 / den
+        const double z2 = (d * d) * (d * d);
+        if (z2 * e6e3 * __builtin_fabs(t) < 1e-17) break;
+    }
+    cosE = C;
+    sinE = S;
+}
+
+// Per-planet constants in the default "P K e w Tp" form (model.py:199-206,
+// model.py:302 n = 2*pi/P).  ok == false exactly where Planet() raises.
+// rv = inv * ((cosE - e) * Kcw - sinE * Ksqsw) + Kecw,  inv = 1 / (1 - e cosE)
+// (= K (cos f cos w - sin f sin w + e cos w), model.py:119-121,170)
+struct PlanetK {
+    double n, Tp, e, Kcw, Ksqsw, Kecw, e6e3, pad;
+};
+
+// param.py:88-105 (NaN passes the '<=' tests, as in the reference)
+__device__ __forceinline__ bool valid_default(double P, double K, double e, double w) {
+    return !(P <= 0.0) && !(K <= 0.0) && !(e < 0.0) && !(e >= 1.0) && (-kPi <= w && w < kPi);
+}
+
+// Conversion to the default parameterisation (param.py:299-362, 198-234).
+// PAR >= 0: compile-time parameterisation (PAR = 0 needs no atan/tan/atan2);
+// PAR = -1: runtime `par`.
+template <int PAR>
+__device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, int par = PAR) {
+    if (PAR >= 0) par = PAR;
+    double P = p5[0], K = p5[1], e, w, Tp;
+    if (par >= 2) {                       // secosw/sesinw -> e, w  (param.py:217-234)
+        double u = p5[2], v = p5[3];
+        e = u * u + v * v;
+        w = atan2(v, u);
+    } else {
+        e = p5[2];
+        w = p5[3];
+    }
+    bool ok = true;
+    if (par == 1 || par == 3) {           // Tc -> Tp  (param.py:198-215)
+        if (e < 0.0 || e >= 1.0) {
+            ok = false;
+            Tp = 0.0;
+        } else {
+            double theta_tc = (kPi / 2) - w;
+            double E = 2 * atan(sqrt((1 - e) / (1 + e)) * tan(theta_tc / 2));
+            double Mc = E - (e * sin(E));
+            Tp = p5[4] - (P / kTwoPi) * Mc;
+        }
+    } else {
+        Tp = p5[4];
+    }
+    ok = ok && valid_default(P, K, e, w);
+    if (!ok) {                            // keep the masked walker's arithmetic finite
+        P = 1.0; e = 0.0; w = 0.0;
+    }
+    pk.n = kTwoPi / P;
+    pk.Tp = Tp;
+    pk.e = e;
+    double sw, cw;
+    sincos_mod(w, sw, cw);
+    pk.Kcw = K * cw;
+    pk.Ksqsw = K * sqrt(1.0 - e * e) * sw;
+    pk.Kecw = K * (e * cw);
+    pk.e6e3 = 6.0 * e * e * e;
+    pk.pad = 0.0;
+    return ok;
+}
+
+__device__ __forceinline__ bool planet_consts(int par, const double *p5, PlanetK &pk) {
+    return planet_consts_t<-1>(p5, pk, par);
+}
+
+// One planet's RV at time t (model.py:327, 119-121, 170).  e == 0 takes the
+// same arithmetic (the solvers return E = M), so there is no branch.
+template <int SOLVER>
+__device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const SC *tab) {
+    const double M = pk.n * (t - pk.Tp);
+    double cE, sE;
+    if (SOLVER == 1) solve_kepler_ref(M, pk.e, cE, sE);
+    else solve_kepler_fast(M, pk.e, pk.e6e3, tab, cE, sE);
+    const double inv = rcp_nr(1.0 - pk.e * cE);
+    return __builtin_fma(inv, __builtin_fma(cE - pk.e, pk.Kcw, -sE * pk.Ksqsw), pk.Kecw);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace rvk

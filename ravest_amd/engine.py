@@ -1,0 +1,121 @@
+"""RVEngine: a device-resident RV log-likelihood handle (wraps rvk_handle).
+
+One engine = one dataset on one MI355X.  ``loglike`` takes a [W, P_full]
+host block in the C-ABI's full-parameter order (include/rvk.h) and returns the
+W per-walker log-likelihoods, -inf where ravest's Planet() would raise
+(fit.py:3622-3627).  ``loglike_device`` is the stream-ordered form on
+device-resident torch tensors (used by bench.py and the multi-GPU path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .param import Parameterisation
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+def _p(a: np.ndarray, ptype=_dp):
+    return a.ctypes.data_as(ptype)
+
+
+class RVEngine:
+    def __init__(self, time, vel, velerr, inst_idx=None, n_inst: int = 1, n_planets: int = 1,
+                 parameterisation="P K e w Tp", t0: float = 0.0, device: int = -1):
+        L = _lib.load()
+        if isinstance(parameterisation, str):
+            parameterisation = Parameterisation(parameterisation)
+        self.parameterisation = parameterisation
+        self.time = np.ascontiguousarray(time, np.float64)
+        self.vel = np.ascontiguousarray(vel, np.float64)
+        self.velerr = np.ascontiguousarray(velerr, np.float64)
+        n = self.time.size
+        if not (self.vel.size == n and self.velerr.size == n):
+            raise ValueError("time, vel and velerr must have the same length")
+        self.inst_idx = (np.zeros(n, np.int32) if inst_idx is None
+                         else np.ascontiguousarray(inst_idx, np.int32))
+        self.n_epochs, self.n_inst, self.n_planets, self.t0 = n, int(n_inst), int(n_planets), float(t0)
+        self.p_full = 5 * self.n_planets + 2 * self.n_inst + 2
+        self._h = L.rvk_create(_p(self.time), _p(self.vel), _p(self.velerr), _p(self.inst_idx, _ip),
+                               n, self.n_inst, self.n_planets, parameterisation.code, self.t0, int(device))
+        if not self._h:
+            raise _lib.RVKError(f"rvk_create failed: {_lib.last_error()}")
+
+    # -- host-buffer path (blocking) -------------------------------------------------
+    def loglike(self, theta: np.ndarray) -> np.ndarray:
+        theta = np.ascontiguousarray(np.atleast_2d(theta), np.float64)
+        if theta.shape[1] < self.p_full:
+            raise ValueError(f"theta rows have {theta.shape[1]} values, need P_full={self.p_full}")
+        out = np.empty(theta.shape[0], np.float64)
+        _lib.check(_lib.load().rvk_loglike(self._h, _p(theta), theta.shape[0], theta.shape[1], _p(out)))
+        return out
+
+    # -- device path (async on the given / current torch stream) ---------------------
+    def loglike_device(self, theta, out, stream=None) -> None:
+        """theta: float64 cuda tensor [W, >=P_full] (contiguous rows); out: float64 [W]."""
+        import torch
+        assert theta.dtype == torch.float64 and out.dtype == torch.float64
+        assert theta.is_cuda and out.is_cuda and theta.stride(1) == 1 and out.is_contiguous()
+        if stream is None:
+            stream = torch.cuda.current_stream(theta.device)
+        _lib.check(_lib.load().rvk_loglike_device(self._h, theta.data_ptr(), theta.shape[0], theta.stride(0),
+                                                  out.data_ptr(), stream.cuda_stream))
+
+    def predict(self, theta: np.ndarray, t, inst=None, planets=None, trend=True, gamma=False) -> np.ndarray:
+        """Posterior-predictive RV [S, T] (sum of the selected planets [+ trend] [+ gamma])."""
+        theta = np.ascontiguousarray(np.atleast_2d(theta), np.float64)
+        t = np.ascontiguousarray(t, np.float64)
+        planets = range(self.n_planets) if planets is None else planets
+        what = 0
+        for p in planets:
+            what |= 1 << int(p)
+        if trend:
+            what |= _lib.PRED_TREND
+        if gamma:
+            what |= _lib.PRED_GAMMA
+        ip = None
+        if inst is not None:
+            inst = np.ascontiguousarray(inst, np.int32)
+            ip = _p(inst, _ip)
+        out = np.empty((theta.shape[0], t.size), np.float64)
+        _lib.check(_lib.load().rvk_predict(self._h, _p(theta), theta.shape[0], theta.shape[1], _p(t), ip,
+                                           t.size, what, _p(out)))
+        return out
+
+    def set_solver(self, solver: int) -> None:
+        """0 = production solver (default); 1 = ravest's Halley iteration restated."""
+        _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_SOLVER, int(solver)))
+
+    def reserve(self, max_walkers: int) -> None:
+        _lib.check(_lib.load().rvk_reserve(self._h, int(max_walkers)))
+
+    def stream_ptr(self) -> int:
+        return _lib.load().rvk_stream(self._h) or 0
+
+    def sync(self) -> None:
+        _lib.check(_lib.load().rvk_sync(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.load().rvk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def solve_kepler(M, e, device: int = -1, solver: int = 0):
+    """cos E, sin E on the GPU for arrays of (M, e) (ravest _solve_kepler, model.py:23-70)."""
+    M = np.ascontiguousarray(M, np.float64)
+    e = np.ascontiguousarray(np.broadcast_to(e, M.shape), np.float64)
+    c = np.empty_like(M)
+    s = np.empty_like(M)
+    _lib.check(_lib.load().rvk_solve_kepler(_p(M), _p(e), M.size, _p(c), _p(s), device, solver))
+    return c, s

@@ -1,0 +1,33 @@
+"""Summarise rocprofv3 --pmc passes for the dominant loglike kernel into profiles/pmc_config<c>.json.
+
+Per-launch values = the counter summed over the kernel's dispatches / number of dispatches.
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KB) reads 1/2 of the bytes of a wide
+coalesced stream -> doubled; WRITE_SIZE (KB) is read as-is.
+"""
+import csv, glob, json, os, sys
+from collections import defaultdict
+
+out_dir, cfg = sys.argv[1], sys.argv[2]
+vals = defaultdict(float)
+disp = defaultdict(set)
+kname = None
+for f in sorted(glob.glob(os.path.join(out_dir, "p*", "**", "*counter_collection.csv"), recursive=True)):
+    for row in csv.DictReader(open(f)):
+        name = row.get("Kernel_Name", "")
+        if "loglike_kernel" not in name:
+            continue
+        kname = name
+        c = row["Counter_Name"]
+        vals[c] += float(row["Counter_Value"])
+        disp[c].add(row.get("Dispatch_Id", row.get("Correlation_Id")))
+per = {c: vals[c] / max(1, len(disp[c])) for c in vals}
+res = {"kernel": kname, "counters_per_launch": per,
+       "source": f"rocprofv3 --pmc passes over `python bench.py --config {cfg} --steps 20 --warmup 5` (tools/pmc.sh)"}
+if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+    res["hbm_bytes_per_launch"] = (2 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
+if "SQ_INSTS_VALU" in per:
+    res["valu_insts_per_launch"] = per["SQ_INSTS_VALU"]
+
+p = os.path.join(out_dir, f"pmc_config{cfg}.json")
+json.dump(res, open(p, "w"), indent=1)
+print(json.dumps(res, indent=1))

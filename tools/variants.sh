@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build A/B variants of librvk.so from the same source (different -D knobs).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/variants
+build() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
+  -o build/variants/librvk_$name.so ravest_amd/csrc/rvk.hip 2>/dev/null & }
+build base
+build lb4 -DRVK_LB_WAVES=4
+build polyseed -DRVK_SEED_HW=0
+build lb4poly -DRVK_LB_WAVES=4 -DRVK_SEED_HW=0
+wait
+ls build/variants
