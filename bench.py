@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--walkers", type=int, default=None, help="walkers per GPU (default: config's, 4096 for cfg 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
+    ap.add_argument("--streams", type=int, default=4, help="independent streams per graph")
     return ap.parse_args()
 
 
@@ -112,57 +114,91 @@ def main():
 
     eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, n_in, n_pl, ds.parameterisation, ds.t0,
                    device=dev.index)
+    eng.reserve(W)                                   # no allocation inside captured launches
     th_d = torch.from_numpy(theta).to(dev)
-    nbuf = 2
-    outs = [torch.empty(W, dtype=torch.float64, device=dev) for _ in range(nbuf)]
-    gath = [torch.empty(W * world, dtype=torch.float64, device=dev) for _ in range(nbuf)] if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
-    works = [None] * nbuf
-
-    def step(k, ev=None):
-        b = k % nbuf
-        if works[b] is not None:       # buffer b's previous all-gather must have read it
-            works[b].wait()
-        if ev is not None:
-            ev[0].record(stream)
-        eng.loglike_device(th_d, outs[b], stream)
-        if ev is not None:
-            ev[1].record(stream)
-        if world > 1:
-            works[b] = dist.all_gather_into_tensor(gath[b], outs[b], async_op=True)
-
-    def drain():
-        for i, w_ in enumerate(works):
-            if w_ is not None:
-                w_.wait()
-                works[i] = None
-
-    for k in range(args.warmup):
-        step(k)
-    drain()
+    # ---- isolated per-launch kernel duration (HIP events on the launch stream) -----------
+    out1 = torch.empty(W, dtype=torch.float64, device=dev)
+    for _ in range(max(1, args.warmup)):
+        eng.loglike_device(th_d, out1, stream)
     torch.cuda.synchronize(dev)
+    ll = out1.cpu().numpy()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+    for a, b in ev:
+        a.record(stream)
+        eng.loglike_device(th_d, out1, stream)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
 
-    # correctness guard on the bench inputs: finite count matches the built-in mask
-    ll = outs[(args.warmup - 1) % nbuf].cpu().numpy() if args.warmup else None
+    # PCIe-inclusive host-buffer path (rvk_loglike: H2D theta, kernel, D2H), for DESIGN.md only
+    eng.loglike(theta)
+    th0 = time.perf_counter()
+    for _ in range(10):
+        eng.loglike(theta)
+    host_ms = (time.perf_counter() - th0) / 10 * 1e3
 
+    # ---- the timed steps: G-step HIP graphs, S independent streams per graph ------------
+    G = max(1, min(args.graph_steps, args.steps))
+    while args.steps % G:                            # time exactly K steps
+        G -= 1
+    S = max(1, args.streams)
+    nset = 2                                         # two output sets: replay r+1 overlaps gather r
+    outs = [torch.empty(G, W, dtype=torch.float64, device=dev) for _ in range(nset)]
+    gath = [torch.empty(world * G * W, dtype=torch.float64, device=dev) for _ in range(nset)] if world > 1 else None
+    graphs = []
+    cap = torch.cuda.Stream(dev)
+    side = [torch.cuda.Stream(dev) for _ in range(S)]
+    for k in range(nset):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            for st in side:
+                st.wait_stream(cap)
+            for j in range(G):
+                eng.loglike_device(th_d, outs[k][j], side[j % S])
+            for st in side:
+                cap.wait_stream(st)
+        graphs.append(g)
+    for g in graphs:                                 # warm replays
+        g.replay()
+    torch.cuda.synchronize(dev)
+    if not np.array_equal(outs[0][G - 1].cpu().numpy(), ll):
+        raise RuntimeError("graph replay result differs from the eager launch")
+
+    works = [None] * nset
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k, ev[k])
-    drain()
+    done = 0
+    r = 0
+    while done < args.steps:
+        k = r % nset
+        if works[k] is not None:                     # set k's previous gather must have read it
+            works[k].wait()
+        graphs[k].replay()
+        if world > 1:
+            works[k] = dist.all_gather_into_tensor(gath[k], outs[k].view(-1), async_op=True)
+        done += G
+        r += 1
+    for k in range(nset):
+        if works[k] is not None:
+            works[k].wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))   # per-launch duration on the kernel's stream
+    steps_run = done
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
+        # the gathered block is every rank's result, bitwise: check rank 0's slice on rank 0
+        mine = gath[(r - 1) % nset].view(world, G, W)[rank, G - 1].cpu().numpy()
+        if not np.array_equal(mine, ll):
+            raise RuntimeError("all-gathered log-probs differ from the local result")
+    args.steps = steps_run
 
     solves = W * n_ep * n_pl * args.steps * world
     value = solves / el
@@ -191,14 +227,17 @@ def main():
                        "parallelism": f"walker-shard x{world}"},
             "walker_evals_per_s": W * world * args.steps / el,
             "kernel_ms": kern_ms,
+            "host_path_ms_per_call": host_ms,
+            "launch": f"{G}-step HIP graphs, {S} streams" + (", 1 all-gather per graph (G steps)" if world > 1 else ""),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "note": "algorithmic bytes = W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY §8(d)); "
-                                 "the kernel is fp64-VALU bound, see 'valu'"},
+                         "achieved_per_step": alg_bytes / (el / args.steps) / 1e9,
+                         "note": "algorithmic bytes = W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY §8(d)) / "
+                                 "isolated per-launch kernel time (HIP events); the kernel is fp64-VALU bound, "
+                                 "see 'valu'"},
             "valu": valu,
         }
-        if ll is not None:
-            line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
+        line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -1,0 +1,66 @@
+"""Walker-block sharding over GPUs (one process per GPU, torch.distributed).
+
+The only exchange on the path: each rank evaluates a
+contiguous block of the W proposals on its own MI355X, then the per-walker
+log-probs are all-gathered (RCCL over xGMI with the "nccl" backend; gloo on
+CPU for tests) so the rank that runs the stretch move sees all W values.
+Every walker is computed wholly on one GPU with a fixed reduction order, so
+results are bitwise identical for any number of ranks.
+
+    lp = LogPosterior(..., device=local_rank)
+    sharded = ShardedLogProbability(lp.log_probability_batch)
+    sampler = EnsembleSampler(W, D, sharded)          # identical proposals on every rank
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_bounds(n: int, world: int, rank: int):
+    """Contiguous [lo, hi) of n items for `rank`; the first n % world ranks get one extra."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+class ShardedLogProbability:
+    def __init__(self, log_prob_batch, group=None, device=None, src: int = 0) -> None:
+        import torch
+        import torch.distributed as dist
+        self.fn = log_prob_batch
+        self.group = group
+        self.dist = dist
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.src = src
+        backend = dist.get_backend(group)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        self.device = device
+
+    def broadcast(self, theta: np.ndarray) -> np.ndarray:
+        """Make rank `src`'s proposal block the block of every rank."""
+        import torch
+        shape = torch.tensor(list(np.shape(theta)) if self.rank == self.src else [0, 0], dtype=torch.int64,
+                             device=self.device)
+        self.dist.broadcast(shape, self.src, group=self.group)
+        buf = (torch.as_tensor(np.ascontiguousarray(theta, np.float64), device=self.device) if self.rank == self.src
+               else torch.empty(tuple(shape.tolist()), dtype=torch.float64, device=self.device))
+        self.dist.broadcast(buf, self.src, group=self.group)
+        return buf.cpu().numpy()
+
+    def __call__(self, theta: np.ndarray) -> np.ndarray:
+        import torch
+        theta = np.atleast_2d(np.asarray(theta, np.float64))
+        n = theta.shape[0]
+        lo, hi = shard_bounds(n, self.world, self.rank)
+        per = -(-n // self.world)                     # padded shard length for all_gather
+        local = np.full(per, np.nan)
+        if hi > lo:
+            local[: hi - lo] = self.fn(theta[lo:hi])
+        t = torch.as_tensor(local, device=self.device)
+        out = torch.empty(per * self.world, dtype=torch.float64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        full = out.cpu().numpy().reshape(self.world, per)
+        return np.concatenate([full[r, : shard_bounds(n, self.world, r)[1] - shard_bounds(n, self.world, r)[0]]
+                               for r in range(self.world)])

@@ -1,0 +1,261 @@
+"""LogPosterior / LogLikelihood / LogPrior: drop-in mirrors of ravest.fit's.
+
+Same constructor arguments, same per-walker semantics and error behaviour as
+src/ravest/fit.py:3228-3691, so emcee, MAP and ravest's Fitter can use them
+unchanged.  The difference is the engine underneath: the likelihood of every
+walker is computed by the HIP kernel behind include/rvk.h (RVEngine), and the
+host-side work (free -> full parameter scatter, jitter check, priors, prior
+conversion, corrections) is vectorised over a whole walker block.
+
+Entry points:
+  * ``log_probability(free_params_dict) -> float``  -- the reference's scalar
+    log_prob_fn (emcee with ``parameter_names``; MAP; single-point callers);
+  * ``log_probability_batch(theta_free[W, D]) -> ndarray[W]`` -- the
+    vectorised drop-in (emcee ``vectorize=True``); ``__call__`` is the same.
+Mask semantics follow fit.py:3461-3495 exactly: jitter < 0, a prior-side
+conversion ValueError, a non-finite log-prior, or an invalid planet give -inf.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Callable, Dict
+
+import numpy as np
+
+from .param import Parameterisation, full_param_names
+from .prior import Uniform, logpdf_vec
+
+
+class LogLikelihood:
+    """fit.py:3529-3660.  ``__call__(params: dict) -> float`` over ALL parameters."""
+
+    def __init__(self, time, vel, velerr, instrument, unique_instruments, t0, planet_letters,
+                 parameterisation: Parameterisation, engine=None, device: int = -1) -> None:
+        self.time = time
+        self.vel = vel
+        self.velerr = velerr
+        self.instrument = instrument
+        self.unique_instruments = unique_instruments
+        self.t0 = t0
+        self.planet_letters = planet_letters
+        self.parameterisation = parameterisation
+        # fit.py:3585-3598
+        _inst_to_idx = {inst: i for i, inst in enumerate(self.unique_instruments)}
+        self._instrument_indices = np.array([_inst_to_idx[inst] for inst in self.instrument], dtype=np.int32)
+        self._gamma_keys = [f"g_{inst}" for inst in self.unique_instruments]
+        self._jitter_keys = [f"jit_{inst}" for inst in self.unique_instruments]
+        self._log_2pi = np.log(2 * np.pi)
+        self._velerr_sq = np.asarray(self.velerr) ** 2
+        self.names = full_param_names(planet_letters, parameterisation, list(unique_instruments))
+        self._engine = engine
+        self._device = device
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            from .engine import RVEngine
+            self._engine = RVEngine(self.time, self.vel, self.velerr, self._instrument_indices,
+                                    len(self.unique_instruments), len(self.planet_letters),
+                                    self.parameterisation, self.t0, device=self._device)
+        return self._engine
+
+    def __getstate__(self):           # picklable (multiprocessing pools), engine rebuilt lazily
+        d = dict(self.__dict__)
+        d["_engine"] = None
+        return d
+
+    def batch(self, theta_full: np.ndarray) -> np.ndarray:
+        """[W, P_full] in ``self.names`` order -> [W] log-likelihoods."""
+        return self.engine.loglike(theta_full)
+
+    def __call__(self, params: Dict[str, float]) -> float:
+        row = np.array([[params[n] for n in self.names]], dtype=np.float64)
+        return float(self.batch(row)[0])
+
+
+class LogPrior:
+    """fit.py:3663-3691."""
+
+    def __init__(self, priors: dict) -> None:
+        self.priors = priors
+
+    def __call__(self, params: Dict[str, float]) -> float:
+        log_prior_probability = 0
+        for param in params:
+            log_prior_probability += self.priors[param](params[param])
+        return log_prior_probability
+
+    def batch(self, cols: Dict[str, np.ndarray]) -> np.ndarray:
+        """Same sum, same key order, vectorised over walkers."""
+        lp = 0
+        for param, col in cols.items():
+            lp = lp + logpdf_vec(self.priors[param], col)
+        return lp
+
+
+class LogPosterior:
+    """fit.py:3228-3526."""
+
+    def __init__(self, planet_letters: list, parameterisation: Parameterisation, priors: dict,
+                 fixed_params: dict, free_params_names: list, time, vel, velerr, instrument,
+                 unique_instruments, t0: float, engine=None, device: int = -1) -> None:
+        self.planet_letters = planet_letters
+        self.parameterisation = parameterisation
+        self.priors = priors
+        self.fixed_params = fixed_params
+        self.free_params_names = free_params_names
+        self.time = time
+        self.vel = vel
+        self.velerr = velerr
+        self.instrument = instrument
+        self.unique_instruments = unique_instruments
+        self.t0 = t0
+        self.log_likelihood = LogLikelihood(time=time, vel=vel, velerr=velerr, instrument=instrument,
+                                            unique_instruments=unique_instruments, t0=t0,
+                                            planet_letters=planet_letters, parameterisation=parameterisation,
+                                            engine=engine, device=device)
+        self.log_prior = LogPrior(self.priors)
+        (self._logprob_jacobian_correction, self._logprob_prior_renorm_correction,
+         self._logprob_correction_breakdown) = self._compute_logprob_corrections()
+        self._build_plan()
+
+    # ---- constant corrections: fit.py:3306-3397 ------------------------------------------
+    def _classify_planet_case(self, letter: str) -> str:
+        if self.parameterisation.log_jacobian_determinant() == 0.0:
+            return "CASE_1"
+        if f"secosw_{letter}" not in self.free_params_names:
+            return "CASE_1"
+        secosw_key, sesinw_key = f"secosw_{letter}", f"sesinw_{letter}"
+        e_key, w_key = f"e_{letter}", f"w_{letter}"
+        if secosw_key in self.priors and sesinw_key in self.priors:
+            sp, vp = self.priors[secosw_key], self.priors[sesinw_key]
+            if (isinstance(sp, Uniform) and isinstance(vp, Uniform) and sp.lower == -1 and sp.upper == 1
+                    and vp.lower == -1 and vp.upper == 1):
+                return "CASE_2"
+            raise NotImplementedError(
+                f"Unsupported priors on (secosw_{letter}, sesinw_{letter}): {sp!r}, {vp!r}. Only Uniform(-1, 1) "
+                "priors on (secosw, sesinw) are supported for evidence-correct log-posterior corrections. A "
+                "separable, rotationally-symmetric belief about eccentricity can always be re-expressed as a "
+                f"prior on e instead - place priors on (e_{letter}, w_{letter}) using one of Ravest's "
+                "eccentricity priors (HalfNormal, Rayleigh, VanEylen19Mixture, Beta, EccentricityUniform, "
+                "TruncatedNormal).")
+        elif e_key in self.priors and w_key in self.priors:
+            return "CASE_3"
+        raise RuntimeError(f"Could not classify log-posterior correction case for planet '{letter}': no priors "
+                           "found on either (secosw, sesinw) or (e, w).")
+
+    def _compute_logprob_corrections(self):
+        log_jac = self.parameterisation.log_jacobian_determinant()
+        total_jacobian, total_renorm, breakdown = 0.0, 0.0, {}
+        for letter in self.planet_letters:
+            case = self._classify_planet_case(letter)
+            jacobian = log_jac if case == "CASE_3" else 0.0
+            renorm = np.log(4.0 / np.pi) if case == "CASE_2" else 0.0
+            total_jacobian += jacobian
+            total_renorm += renorm
+            breakdown[letter] = {"case": case, "jacobian": jacobian, "renorm": renorm}
+            logging.info(f"Planet {letter}: log-posterior correction case {case} "
+                         f"(jacobian={jacobian}, renorm={renorm})")
+        return total_jacobian, total_renorm, breakdown
+
+    # ---- vectorisation plan (built once) --------------------------------------------------
+    def _build_plan(self) -> None:
+        names = self.log_likelihood.names
+        self._names = names
+        self._template = np.array([float(self.fixed_params[n]) if n in self.fixed_params else np.nan
+                                   for n in names])
+        self._free_idx = np.array([names.index(n) for n in self.free_params_names], dtype=np.int64)
+        missing = [n for n in names if n not in self.fixed_params and n not in self.free_params_names]
+        if missing:
+            raise KeyError(f"parameters neither fixed nor free: {missing}")
+        self._jit_idx = np.array([names.index(f"jit_{inst}") for inst in self.unique_instruments])
+        prior_keys = set(self.priors.keys())
+        self._case3 = prior_keys != set(self.free_params_names)     # fit.py:3418-3423
+        pars = self.parameterisation.pars
+        # prior-evaluation key order, exactly the dict order of fit.py:3426-3444
+        order = [k for k in self.free_params_names if k in prior_keys]
+        if self._case3:
+            for L in self.planet_letters:
+                for dp in ("P", "K", "e", "w", "Tp"):
+                    key = f"{dp}_{L}"
+                    if key in prior_keys and key not in order:
+                        order.append(key)
+        self._prior_order = order
+        self._planet_cols = {L: {par: names.index(f"{par}_{L}") for par in pars} for L in self.planet_letters}
+
+    def _full(self, theta_free: np.ndarray) -> np.ndarray:
+        full = np.repeat(self._template[None, :], theta_free.shape[0], axis=0)
+        full[:, self._free_idx] = theta_free
+        return full
+
+    def _log_prior_batch(self, theta_free: np.ndarray, full: np.ndarray):
+        """Vectorised fit.py:3475-3482: returns (lp, conversion_ok)."""
+        free_col = {n: theta_free[:, i] for i, n in enumerate(self.free_params_names)}
+        ok = np.ones(theta_free.shape[0], bool)
+        if not self._case3:
+            cols = {k: free_col[k] for k in self._prior_order}
+        else:
+            conv = {}
+            for L, cmap in self._planet_cols.items():
+                d, okL = self.parameterisation.to_default_vec({par: full[:, j] for par, j in cmap.items()})
+                ok &= okL
+                for dp, v in d.items():
+                    conv[f"{dp}_{L}"] = v
+            cols = {}
+            for k in self._prior_order:
+                # planet default keys take the converted value (fit.py:3441-3444 overwrite in place)
+                cols[k] = conv[k] if k in conv else free_col[k]
+        with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+            lp = self.log_prior.batch(cols)
+        lp = np.broadcast_to(np.asarray(lp, dtype=np.float64), (theta_free.shape[0],))
+        return lp, ok
+
+    # ---- public API -----------------------------------------------------------------------
+    def log_probability_batch(self, theta_free) -> np.ndarray:
+        theta_free = np.ascontiguousarray(np.atleast_2d(np.asarray(theta_free, dtype=np.float64)))
+        if theta_free.shape[1] != len(self.free_params_names):
+            raise ValueError(f"expected {len(self.free_params_names)} free parameters, got {theta_free.shape[1]}")
+        full = self._full(theta_free)
+        dead = np.any(full[:, self._jit_idx] < 0, axis=1)                 # fit.py:3465-3468
+        lp, conv_ok = self._log_prior_batch(theta_free, full)             # fit.py:3475-3480
+        dead |= ~conv_ok
+        dead |= ~np.isfinite(lp)                                          # fit.py:3481-3482
+        out = np.full(theta_free.shape[0], -np.inf)
+        live = ~dead
+        if live.any():
+            ll = self.log_likelihood.batch(full[live])                    # fit.py:3485
+            logprob = ll + lp[live]                                       # fit.py:3492-3494
+            logprob = logprob + self._logprob_jacobian_correction
+            logprob = logprob + self._logprob_prior_renorm_correction
+            out[live] = logprob
+        return out
+
+    __call__ = log_probability_batch
+
+    def log_probability(self, free_params_dict: Dict[str, float]) -> float:
+        row = np.array([[free_params_dict[n] for n in self.free_params_names]], dtype=np.float64)
+        return float(self.log_probability_batch(row)[0])
+
+    def _convert_params_for_prior_evaluation(self, free_params_dict: Dict[str, float]) -> Dict[str, float]:
+        """fit.py:3399-3446 (scalar form, kept for API parity)."""
+        prior_keys = set(self.priors.keys())
+        if prior_keys == set(self.free_params_names):
+            return free_params_dict
+        params_for_prior = {k: v for k, v in free_params_dict.items() if k in prior_keys}
+        all_params = self.fixed_params | free_params_dict
+        for L in self.planet_letters:
+            planet_params = {par: all_params[f"{par}_{L}"] for par in self.parameterisation.pars}
+            default_params = self.parameterisation.convert_pars_to_default_parameterisation(planet_params)
+            for dp, value in default_params.items():
+                key = f"{dp}_{L}"
+                if key in prior_keys:
+                    params_for_prior[key] = value
+        return params_for_prior
+
+    def _negative_log_probability_for_MAP(self, free_params_vals) -> float:
+        """fit.py:3497-3526."""
+        logprob = self.log_probability(dict(zip(self.free_params_names, free_params_vals)))
+        neg = -logprob
+        if not np.isfinite(neg):
+            return 1e30
+        return neg

@@ -1,0 +1,77 @@
+"""The C oracle (oracle/rv_oracle.c) pinned against the reference's own fixtures and the
+golden vectors generated from the reference (tools/gen_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from ravest_amd.param import PARAMETERISATION_CODE
+from tests._golden import GOLDEN, ORACLE_RTOL, assert_ll_close, load_case, logpost_cases
+
+
+def test_kepler_grid_bitwise():
+    g = np.load(f"{GOLDEN}/kepler_grid.npz")
+    c, s, it = oracle.solve_kepler(g["M"], g["e"])
+    # same Halley arithmetic, same libm sin/cos as the interpreted reference
+    assert np.max(np.abs(c - g["cosE"])) <= 1e-16 and np.max(np.abs(s - g["sinE"])) <= 1e-16
+    assert it.max() <= 8     # SURVEY.md §7 hard part 3: e <= 0.9999 converges in <= 8 iterations
+
+
+def test_compute_rv_fixture():
+    g = np.load(f"{GOLDEN}/compute_rv.npz")
+    for (e, K, w), M, ref in zip(g["params"], g["M"], g["rv"]):
+        np.testing.assert_allclose(oracle.compute_rv(M, e, K, w), ref, rtol=0, atol=1e-13 * K)
+
+
+@pytest.mark.parametrize("fname,p", [("rv1.txt", [13.2, 27, 0.2, 0.9 * np.pi, 2]),
+                                     ("rv2.txt", [1.5, 10, 0, np.pi / 2, 0])])
+def test_reference_rv_fixtures(fname, p):
+    """Reference tests/test_model.py:99-108 on the reference's own data files."""
+    t = np.arange(0, 100, 0.1)
+    rv = oracle.planet_rv(0, np.array(p, float), t)
+    ref = np.loadtxt(f"{GOLDEN}/{fname}")
+    np.testing.assert_allclose(rv, ref, rtol=1e-6, atol=1e-12)
+    assert np.max(np.abs(rv - ref)) <= 1e-12
+
+
+def test_planet_rv_all_parameterisations():
+    g = np.load(f"{GOLDEN}/planet_rv.npz")
+    for code in range(4):
+        t, prm, ref = g[f"t_{code}"], g[f"params_{code}"], g[f"rv_{code}"]
+        for p5, r in zip(prm, ref):
+            rv = oracle.planet_rv(code, p5, t)
+            if np.isnan(r).all():
+                assert rv is None
+            else:
+                np.testing.assert_allclose(rv, r, rtol=0, atol=1e-12 * abs(p5[1]))
+
+
+@pytest.mark.parametrize("tp,e,w,tc", [(0, 0.3, 3 * np.pi / 8, 0.32487717871429983),
+                                       (3.33, 0.51, -np.pi / 5, 5.200496945307864),
+                                       (5, 0.69, 0, 5.493187444825672), (8.2, 0.8, np.pi / 7, 8.34625216953673)])
+def test_tc_tp_reference_goldens(tp, e, w, tc):
+    """Reference tests/test_param.py:59-91 (P = 10)."""
+    assert np.isclose(oracle.tc_to_tp(tc, 10.0, e, w), tp)
+
+
+def test_tc_to_tp_grid():
+    g = np.load(f"{GOLDEN}/convert.npz")
+    tp = np.array([oracle.tc_to_tp(*a) for a in zip(g["tc"], g["per"], g["e"], g["w"])])
+    np.testing.assert_allclose(tp, g["tp"], rtol=1e-14, atol=1e-12)
+    assert oracle.tc_to_tp(1.0, 10.0, 1.0, 0.3) is None and oracle.tc_to_tp(1.0, 10.0, -0.1, 0.3) is None
+
+
+def test_pairwise_sum_matches_numpy():
+    rng = np.random.default_rng(0)
+    for n in [0, 1, 5, 7, 8, 9, 127, 128, 129, 153, 256, 1000, 1024, 4097]:
+        a = rng.standard_normal(n) * rng.uniform(1, 1e3, n)
+        assert oracle.pairwise_sum(a) == np.sum(a)
+
+
+@pytest.mark.parametrize("name", logpost_cases())
+def test_loglike_vs_reference(name):
+    case = load_case(name)
+    m = case["meta"]
+    ll, _ = oracle.loglike(case["time"], case["vel"], case["velerr"], case["inst_idx"], len(m["unique_instruments"]),
+                           len(m["planet_letters"]), PARAMETERISATION_CODE[m["parameterisation"]], m["t0"],
+                           case["theta_full"])
+    assert_ll_close(ll, case["log_like"], rtol=ORACLE_RTOL, what=name)
