@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-FP64_VALU_PEAK = 256 * 4 * 16 * 2.4e9   # lane-ops/s: 256 CU x 4 SIMD x 16 fp64 lanes/clk x 2.4 GHz
+FP64_VECTOR_PEAK_TF = 78.6     # MI355X FP64 vector peak (spec; half the FP32 vector rate)
 BYTES_PER_WALKER_EPOCH = 28    # t, v, sigma fp64 + int32 inst
 
 
@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
-    ap.add_argument("--streams", type=int, default=4, help="independent streams per graph")
+    ap.add_argument("--streams", type=int, default=1, help="independent streams per graph")
     return ap.parse_args()
 
 
@@ -94,10 +94,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RVK_BENCH_BACKEND=gloo: rehearsal of the N>1 path on a 1-GPU box (ranks share cuda:0, the
+    # all-gather goes through host memory); the real multi-GPU run uses RCCL ("nccl").
+    backend = os.environ.get("RVK_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -130,7 +137,7 @@ def main():
         eng.loglike_device(th_d, out1, stream)
         b.record(stream)
     torch.cuda.synchronize(dev)
-    kern_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    eager_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))   # includes event/launch overhead
 
     # PCIe-inclusive host-buffer path (rvk_loglike: H2D theta, kernel, D2H), for DESIGN.md only
     eng.loglike(theta)
@@ -167,6 +174,7 @@ def main():
         raise RuntimeError("graph replay result differs from the eager launch")
 
     works = [None] * nset
+    rep_ev = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -177,9 +185,17 @@ def main():
         k = r % nset
         if works[k] is not None:                     # set k's previous gather must have read it
             works[k].wait()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)                             # the graph is replayed on `stream`
         graphs[k].replay()
-        if world > 1:
+        b.record(stream)
+        rep_ev.append((a, b))
+        if world > 1 and backend == "nccl":
             works[k] = dist.all_gather_into_tensor(gath[k], outs[k].view(-1), async_op=True)
+        elif world > 1:
+            hb = torch.empty(world * G * W, dtype=torch.float64)
+            dist.all_gather_into_tensor(hb, outs[k].view(-1).cpu())
+            gath[k].copy_(hb)
         done += G
         r += 1
     for k in range(nset):
@@ -190,8 +206,10 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     steps_run = done
+    # average kernel duration inside the timed region: G back-to-back launches per replay
+    kern_ms = float(sum(a.elapsed_time(b) for a, b in rep_ev)) / steps_run
     if world > 1:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
         # the gathered block is every rank's result, bitwise: check rank 0's slice on rank 0
@@ -210,11 +228,14 @@ def main():
         valu = None
         if pmc:
             traffic = pmc.get("hbm_bytes_per_launch")
-            if pmc.get("valu_insts_per_launch"):
-                # wave64 fp64 VALU instruction = 64 lane-ops; FP64_VALU_PEAK in lane-ops/s
-                ops = pmc["valu_insts_per_launch"] * 64
-                valu = {"achieved_lane_ops_per_s": ops / (kern_ms * 1e-3), "peak_fp64_lane_ops_per_s": FP64_VALU_PEAK,
-                        "frac": ops / (kern_ms * 1e-3) / FP64_VALU_PEAK, "source": pmc.get("source")}
+            c = pmc.get("counters_per_launch", {})
+            if c.get("SQ_INSTS_VALU_FLOPS_FP64"):
+                # FLOPS counters count per wave instruction (FMA = 2): x64 lanes -> FLOP per launch
+                f64 = c["SQ_INSTS_VALU_FLOPS_FP64"] * 64 / (kern_ms * 1e-3) / 1e12
+                f32 = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * 64 / (kern_ms * 1e-3) / 1e12
+                valu = {"fp64_tflops": f64, "peak_fp64_tflops": FP64_VECTOR_PEAK_TF, "frac": f64 / FP64_VECTOR_PEAK_TF,
+                        "fp32_tflops": f32, "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
+                        "source": pmc.get("source") + " (profiles/pmc_config%d.json)" % args.config}
         line = {
             "metric": "walker-log-prob evals/sec (= Kepler solves/sec) at 1/2/4/8 MI355X",
             "value": value, "unit": "Kepler solves/s", "n_gpus": world, "steps": args.steps,
@@ -227,14 +248,15 @@ def main():
                        "parallelism": f"walker-shard x{world}"},
             "walker_evals_per_s": W * world * args.steps / el,
             "kernel_ms": kern_ms,
+            "eager_event_ms": eager_ms,
             "host_path_ms_per_call": host_ms,
             "launch": f"{G}-step HIP graphs, {S} streams" + (", 1 all-gather per graph (G steps)" if world > 1 else ""),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "achieved_per_step": alg_bytes / (el / args.steps) / 1e9,
                          "note": "algorithmic bytes = W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY §8(d)) / "
-                                 "isolated per-launch kernel time (HIP events); the kernel is fp64-VALU bound, "
-                                 "see 'valu'"},
+                                 "average kernel duration (HIP events around each G-launch graph replay in the "
+                                 "timed region / G); the kernel is fp64-VALU bound, see 'valu'"},
             "valu": valu,
         }
         line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())

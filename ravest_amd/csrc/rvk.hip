@@ -31,8 +31,11 @@ using namespace rvk;
 namespace {
 
 constexpr int kBlock = 256;          // 4 waves
+#ifndef RVK_TAB_LDS
+#define RVK_TAB_LDS 1                 // sin/cos table staged in LDS (1) or read through L1 (0)
+#endif
 #ifndef RVK_LB_WAVES
-#define RVK_LB_WAVES 1                // __launch_bounds__ min waves per SIMD for loglike_kernel
+#define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
 constexpr int kWavesPerBlock = kBlock / 64;
 
@@ -72,21 +75,24 @@ struct PassCfg {
 };
 
 template <int NP, bool MULTI, int SOLVER, bool FUSED>
-__global__ __launch_bounds__(kBlock, RVK_LB_WAVES) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
+__global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
                                                          long long stride, int wb, const PlanetK *__restrict__ ws,
                                                          const int *__restrict__ ws_ok, double *__restrict__ out) {
     constexpr int WB = PassCfg<NP>::WB;
     __shared__ PlanetK pks[WB][NP];
-    __shared__ int okw[WB];
+    __shared__ int okp[WB][NP];
+#if RVK_TAB_LDS
     __shared__ SC tab[kTabN];
     for (int i = threadIdx.x; i < kTabN; i += kBlock) tab[i] = d.tab[i];
+#else
+    const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
+#endif
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
-        if (threadIdx.x < WB) okw[threadIdx.x] = 1;
-        __syncthreads();
+        // prep (the table fill above lands under the same barrier)
         for (int k = threadIdx.x; k < nb * NP; k += kBlock) {
             const int j = k / NP, p = k - j * NP;
             const long long w = base + j;
@@ -99,13 +105,16 @@ __global__ __launch_bounds__(kBlock, RVK_LB_WAVES) void loglike_kernel(EpochData
                 ok = ws_ok[w * NP + p] != 0;
             }
             pks[j][p] = pk;
-            if (!ok) okw[j] = 0;
+            okp[j][p] = ok;
         }
         __syncthreads();
         for (int j = wv; j < nb; j += kWavesPerBlock) {
             const long long w = base + j;
             const double *row = theta + w * stride;
-            if (!okw[j]) {
+            bool all_ok = true;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) all_ok &= okp[j][p] != 0;
+            if (!all_ok) {
                 if (lane == 0) out[w] = -INFINITY;
                 continue;
             }
@@ -155,7 +164,7 @@ __global__ __launch_bounds__(kBlock, RVK_LB_WAVES) void loglike_kernel(EpochData
             double tot = wave_sum(chi2 + lsum);
             if (lane == 0) out[w] = -0.5 * (tot + (double)n_epochs * kLog2Pi);
         }
-        __syncthreads();   // pks/okw are rewritten by the next pass
+        if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // pks/okp are rewritten next pass
     }
 }
 

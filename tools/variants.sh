@@ -6,8 +6,8 @@ mkdir -p build/variants
 build() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
   -o build/variants/librvk_$name.so ravest_amd/csrc/rvk.hip 2>/dev/null & }
 build base
-build lb4 -DRVK_LB_WAVES=4
+build tabg -DRVK_TAB_LDS=0
+build lb3 -DRVK_LB_WAVES=3
 build polyseed -DRVK_SEED_HW=0
-build lb4poly -DRVK_LB_WAVES=4 -DRVK_SEED_HW=0
 wait
 ls build/variants
