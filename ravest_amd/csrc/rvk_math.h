@@ -16,9 +16,11 @@
 //    values within the stated fp64 tolerance:
 //      1. r = M reduced to [-pi, pi] (Cody-Waite, FMA);
 //      2. fp32 Halley seed from E0 = r with the hardware v_sin_f32/v_cos_f32
-//         (accurate fp32 polynomials when e > 0.95, wave-uniform branch);
-//         per-lane exit at |dE| < 2e-5, at most 8 iterations -- the large early
-//         steps cost fp32 issue slots, not fp64 ones;
+//         (accurate fp32 polynomials when e > 0.95, wave-uniform branch),
+//         started from the series E0 = r + e sin r (1 + e cos r); per-lane exit
+//         once an update is < 1e-2 (Halley is cubic: the error after it is
+//         ~K d^3, ~1e-6); at most 8 iterations.  The large early steps cost
+//         fp32 issue slots, not fp64 ones;
 //      3. sin/cos of the fp32 root in fp64 from an LDS table of sin/cos at
 //         j*pi/128 plus a degree-7/8 Taylor rotation (|d| <= pi/256);
 //      4. Householder order-3 steps (quartic convergence) with sin/cos carried
@@ -156,26 +158,43 @@ __device__ __forceinline__ void sincos_tab(double E, const SC *tab, double &S, d
     C = __builtin_fma(sc.c, cm, __builtin_fma(-sc.s, sd, sc.c));
 }
 
+#ifndef RVK_SEED_START
+#define RVK_SEED_START 1      // 0: E0 = r (ravest's seed); 1: E0 = r + e sin r (1 + e cos r)
+#endif
+#ifndef RVK_SEED_THR
+#define RVK_SEED_THR 1e-2f    // exit once a Halley update is below this (error ~ K d^3 after it)
+#endif
+
+template <bool PRECISE32>
+__device__ __forceinline__ void sincos_seed(float x, float &s, float &c) {
+    if (PRECISE32) {
+        sincos_f32(x, s, c);
+    } else {
+        const float rev = x * 0.159154943f;   // v_sin/v_cos take revolutions
+        s = __builtin_amdgcn_sinf(rev);
+        c = __builtin_amdgcn_cosf(rev);
+    }
+}
+
 template <bool PRECISE32>
 __device__ __forceinline__ float seed_f32(float rf, float ef) {
     float Ef = rf;
+    if (RVK_SEED_START == 1) {               // second-order series starter: ~1 Halley step fewer
+        float s0, c0;
+        sincos_seed<PRECISE32>(rf, s0, c0);
+        Ef = __builtin_fmaf(ef * s0, __builtin_fmaf(ef, c0, 1.0f), rf);
+    }
 #pragma unroll 1
     for (int it = 0; it < 8; ++it) {
         float s, c;
-        if (PRECISE32) {
-            sincos_f32(Ef, s, c);
-        } else {
-            const float x = Ef * 0.159154943f;   // v_sin/v_cos take revolutions
-            s = __builtin_amdgcn_sinf(x);
-            c = __builtin_amdgcn_cosf(x);
-        }
+        sincos_seed<PRECISE32>(Ef, s, c);
         const float f = Ef - ef * s - rf;
         const float fp = 1.0f - ef * c;
         const float fpp = ef * s;
         const float den = __builtin_fmaf(-0.5f * f, fpp, fp * fp);
         const float d = f * fp * __builtin_amdgcn_rcpf(den);
         Ef -= d;
-        if (__builtin_fabsf(d) < 2e-5f) break;
+        if (__builtin_fabsf(d) < RVK_SEED_THR) break;
     }
     return Ef;
 }
