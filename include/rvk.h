@@ -80,9 +80,9 @@ int rvk_loglike(rvk_handle *h, const double *theta, int64_t n_walkers, int64_t r
 int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t n_walkers,
                        int64_t row_stride, double *d_out, void *stream);
 
-/* Pre-size the handle's device workspace for up to max_walkers per call, so
- * that rvk_loglike_device never allocates (required before capturing it in a
- * HIP graph).  Only the Tc / secosw parameterisations use a workspace. */
+/* Pre-size any device workspace for up to max_walkers per call, so that
+ * rvk_loglike_device never allocates inside a captured HIP graph.  (The current
+ * kernels need none: this returns RVK_OK; call it anyway before capture.) */
 int rvk_reserve(rvk_handle *h, int64_t max_walkers);
 
 /* Posterior predictive: out[s][j] = sum of the selected components for sample

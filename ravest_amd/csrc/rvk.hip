@@ -31,6 +31,9 @@ using namespace rvk;
 namespace {
 
 constexpr int kBlock = 256;          // 4 waves
+#ifndef RVK_CHI_NR2
+#define RVK_CHI_NR2 0
+#endif
 #ifndef RVK_TAB_LDS
 #define RVK_TAB_LDS 1                 // sin/cos table staged in LDS (1) or read through L1 (0)
 #endif
@@ -47,6 +50,7 @@ struct EpochData {
     const int32_t *inst;  // instrument index (fit.py:3586)
     const SC *tab;        // sin/cos table (rvk_math.h, kTabN entries)
     double t0;            // Trend reference time (model.py:486,491)
+    int par;              // parameterisation code (RVK_PAR_*)
 };
 
 // Copy the sin/cos table into LDS (whole block; one barrier, before any
@@ -60,11 +64,10 @@ __device__ __forceinline__ void load_tab(SC *lds, const SC *__restrict__ g) {
 // (contiguous).  Each pass:
 //   1. prep, lane-parallel over (walker, planet): thread k builds PlanetK for
 //      walker k/NP, planet k%NP into LDS -- one conversion latency per pass
-//      instead of one per walker, and no planet state lives in registers;
-//        FUSED = true : "P K e w Tp" computed here (IEEE div, sqrt, sincos; no
-//                       OCML atan/tan, so the kernel keeps its register budget);
-//        FUSED = false: copied from the prep kernel's workspace (Tc and
-//                       secosw/sesinw need atan/tan/atan2);
+//      instead of one per walker, and no planet state lives in registers.  The
+//      conversion (param.py:198-234, 299-362) is an out-of-line call with
+//      register-light atan/atan2/tan (rvk_math.h), so it does not set the
+//      epoch loop's VGPR budget;
 //   2. __syncthreads (the first pass also covers the sin/cos table fill);
 //   3. wave wv evaluates walkers wv, wv+4, ... of the pass: lanes stride the
 //      epochs, planet constants are re-read from LDS with a wave-uniform
@@ -74,21 +77,28 @@ struct PassCfg {
     static constexpr int WB = (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
 };
 
-template <int NP, bool MULTI, int SOLVER, bool FUSED>
+template <int NP, bool MULTI, int SOLVER, bool TP>
 __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
-                                                         long long stride, int wb, const PlanetK *__restrict__ ws,
-                                                         const int *__restrict__ ws_ok, double *__restrict__ out) {
+                                                         long long stride, int wb, double *__restrict__ out) {
     constexpr int WB = PassCfg<NP>::WB;
     __shared__ PlanetK pks[WB][NP];
     __shared__ int okp[WB][NP];
+    const int lane = threadIdx.x & 63;
+    // Epoch data does not depend on the walker: this lane's first epoch is loaded once,
+    // before anything else, so its latency hides under the table fill and the prep.
+    double t_1 = 0.0, v_1 = 0.0, s_1 = 1.0;
+    int i_1 = 0;
+    if (lane < n_epochs) {
+        t_1 = d.t[lane]; v_1 = d.vel[lane]; s_1 = d.s2[lane];
+        if (MULTI) i_1 = d.inst[lane];
+    }
 #if RVK_TAB_LDS
     __shared__ SC tab[kTabN];
     for (int i = threadIdx.x; i < kTabN; i += kBlock) tab[i] = d.tab[i];
 #else
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
 #endif
-    const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
@@ -97,13 +107,9 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             const int j = k / NP, p = k - j * NP;
             const long long w = base + j;
             PlanetK pk;
-            bool ok;
-            if (FUSED) {
-                ok = planet_consts_t<0>(theta + w * stride + 5 * p, pk);
-            } else {
-                pk = ws[w * NP + p];
-                ok = ws_ok[w * NP + p] != 0;
-            }
+            // "P K e w Tp" inline (no call, no scratch); the others out of line
+            const bool ok = TP ? planet_consts_t<0>(theta + w * stride + 5 * p, pk)
+                               : planet_consts(d.par, theta + w * stride + 5 * p, pk);
             pks[j][p] = pk;
             okp[j][p] = ok;
         }
@@ -126,12 +132,8 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             int expo = 0;
             // software pipeline: the next epoch's data is in flight during this epoch's solve
             int i = lane;
-            double tn = 0.0, vn = 0.0, sn = 1.0;
-            int in_ = 0;
-            if (i < n_epochs) {
-                tn = d.t[i]; vn = d.vel[i]; sn = d.s2[i];
-                if (MULTI) in_ = d.inst[i];
-            }
+            double tn = t_1, vn = v_1, sn = s_1;
+            int in_ = i_1;
             for (; i < n_epochs; i += 64) {
                 const double t = tn, vel = vn, s2b = sn;
                 const int ii = in_;
@@ -154,7 +156,11 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                 rv += gam;
                 const double s2 = s2b + jj;
                 const double r = rv - vel;
+#if RVK_CHI_NR2
                 chi2 = __builtin_fma(r * r, rcp_nr(s2), chi2);
+#else
+                chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);   // <= 2.2e-15 relative per term
+#endif
                 prod *= s2;
                 int ex;
                 prod = __builtin_frexp(prod, &ex);
@@ -166,21 +172,6 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
         }
         if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // pks/okp are rewritten next pass
     }
-}
-
-// Per-(walker, planet) conversion for the Tc / secosw parameterisations
-// (param.py:198-234, 299-362), one thread each; feeds loglike_kernel<..., false>.
-__global__ __launch_bounds__(256) void prep_kernel(int par, int np, const double *__restrict__ theta,
-                                                   long long n_walkers, long long stride, PlanetK *__restrict__ ws,
-                                                   int *__restrict__ ws_ok) {
-    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n_walkers * np) return;
-    long long w = idx / np;
-    int p = (int)(idx - w * np);
-    PlanetK pk;
-    bool ok = planet_consts(par, theta + w * stride + 5 * p, pk);
-    ws[idx] = pk;
-    ws_ok[idx] = ok ? 1 : 0;
 }
 
 // Posterior predictive (fit.py:2690-2939): one wave per sample, lanes over times.
@@ -255,16 +246,15 @@ int fail(int code, const std::string &msg) {
             return fail(RVK_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
     } while (0)
 
-typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long,
-                                 const PlanetK *, const int *, double *);
+typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long, double *);
 
 // Grid: one pass per block when W is small (4 walkers per block = 1 per wave);
 // for large W at most kMaxBlocks blocks, each looping over passes of <= WB walkers.
 constexpr long long kMaxBlocks = 2048;
 
-template <int NP, bool MULTI, int SOLVER, bool FUSED>
+template <int NP, bool MULTI, int SOLVER, bool TP>
 void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
-               const PlanetK *ws, const int *ws_ok, double *out) {
+               double *out) {
     constexpr int WB = PassCfg<NP>::WB;
     long long blocks = (W + kWavesPerBlock - 1) / kWavesPerBlock;
     int wb = kWavesPerBlock;
@@ -275,33 +265,33 @@ void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, lon
         blocks = (W + wb - 1) / wb;
         if (blocks > kMaxBlocks) blocks = kMaxBlocks;
     }
-    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, FUSED>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
-                       ni, th, W, stride, wb, ws, ws_ok, out);
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n, ni,
+                       th, W, stride, wb, out);
 }
 
-template <bool MULTI, int SOLVER, bool FUSED>
+template <bool MULTI, int SOLVER, bool TP>
 loglike_launch_t pick_ll_s(int np) {
     switch (np) {
-        case 1: return launch_ll<1, MULTI, SOLVER, FUSED>;
-        case 2: return launch_ll<2, MULTI, SOLVER, FUSED>;
-        case 3: return launch_ll<3, MULTI, SOLVER, FUSED>;
-        case 4: return launch_ll<4, MULTI, SOLVER, FUSED>;
-        case 5: return launch_ll<5, MULTI, SOLVER, FUSED>;
-        case 6: return launch_ll<6, MULTI, SOLVER, FUSED>;
-        case 7: return launch_ll<7, MULTI, SOLVER, FUSED>;
-        case 8: return launch_ll<8, MULTI, SOLVER, FUSED>;
+        case 1: return launch_ll<1, MULTI, SOLVER, TP>;
+        case 2: return launch_ll<2, MULTI, SOLVER, TP>;
+        case 3: return launch_ll<3, MULTI, SOLVER, TP>;
+        case 4: return launch_ll<4, MULTI, SOLVER, TP>;
+        case 5: return launch_ll<5, MULTI, SOLVER, TP>;
+        case 6: return launch_ll<6, MULTI, SOLVER, TP>;
+        case 7: return launch_ll<7, MULTI, SOLVER, TP>;
+        case 8: return launch_ll<8, MULTI, SOLVER, TP>;
         default: return nullptr;
     }
 }
 
-template <int SOLVER, bool FUSED>
-loglike_launch_t pick_ll_f(int np, bool multi) {
-    return multi ? pick_ll_s<true, SOLVER, FUSED>(np) : pick_ll_s<false, SOLVER, FUSED>(np);
+template <int SOLVER, bool TP>
+loglike_launch_t pick_ll_t(int np, bool multi) {
+    return multi ? pick_ll_s<true, SOLVER, TP>(np) : pick_ll_s<false, SOLVER, TP>(np);
 }
 
-loglike_launch_t pick_ll(int np, bool multi, int solver, bool fused) {
-    if (solver == 1) return fused ? pick_ll_f<1, true>(np, multi) : pick_ll_f<1, false>(np, multi);
-    return fused ? pick_ll_f<0, true>(np, multi) : pick_ll_f<0, false>(np, multi);
+loglike_launch_t pick_ll(int np, bool multi, int solver, bool tp) {
+    if (solver == 1) return tp ? pick_ll_t<1, true>(np, multi) : pick_ll_t<1, false>(np, multi);
+    return tp ? pick_ll_t<0, true>(np, multi) : pick_ll_t<0, false>(np, multi);
 }
 
 int check_gfx950(int dev) {
@@ -348,10 +338,6 @@ struct rvk_handle {
     // scratch for the host-buffer entry points
     double *d_theta = nullptr, *d_out = nullptr;
     size_t cap_theta = 0, cap_out = 0;
-    // prep-kernel workspace (parameterisations other than "P K e w Tp")
-    PlanetK *d_ws = nullptr;
-    int *d_ws_ok = nullptr;
-    long long cap_ws = 0;   // walkers
     loglike_launch_t launch = nullptr;
     int solver = 0;
 };
@@ -388,8 +374,6 @@ static void free_handle(rvk_handle *h) {
     (void)hipFree(h->d_inst);
     (void)hipFree(h->d_theta);
     (void)hipFree(h->d_out);
-    (void)hipFree(h->d_ws);
-    (void)hipFree(h->d_ws_ok);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -483,23 +467,11 @@ static int check_rows(rvk_handle *h, int64_t W, int64_t stride) {
     return RVK_OK;
 }
 
-static int reserve_ws(rvk_handle *h, long long W) {
-    if (h->par == RVK_PAR_PKEWTP || W <= h->cap_ws) return RVK_OK;
-    (void)hipFree(h->d_ws);
-    (void)hipFree(h->d_ws_ok);
-    h->d_ws = nullptr;
-    h->d_ws_ok = nullptr;
-    h->cap_ws = 0;
-    HIPCHK(hipMalloc(&h->d_ws, sizeof(PlanetK) * (size_t)W * h->n_planets));
-    HIPCHK(hipMalloc(&h->d_ws_ok, sizeof(int) * (size_t)W * h->n_planets));
-    h->cap_ws = W;
-    return RVK_OK;
-}
-
 int rvk_reserve(rvk_handle *h, int64_t max_walkers) {
+    // The launch path allocates nothing (no workspace since the conversion moved into the
+    // kernel's prep phase); kept so callers can size for graph capture unconditionally.
     if (!h || max_walkers < 0) return fail(RVK_E_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(h->device));
-    return reserve_ws(h, max_walkers);
+    return RVK_OK;
 }
 
 int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t W, int64_t stride, double *d_out,
@@ -510,14 +482,8 @@ int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t W, int64_t 
     if (!d_theta || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     hipStream_t st = (hipStream_t)stream;   // used as given: NULL is HIP's default stream
     HIPCHK(hipSetDevice(h->device));
-    if ((rc = reserve_ws(h, W))) return rc;
-    if (h->par != RVK_PAR_PKEWTP) {
-        long long items = W * (long long)h->n_planets;
-        hipLaunchKernelGGL(prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, h->par,
-                           h->n_planets, d_theta, (long long)W, (long long)stride, h->d_ws, h->d_ws_ok);
-    }
-    EpochData d{h->d_t, h->d_vel, h->d_s2, h->d_inst, h->d_tab, h->t0};
-    h->launch(st, d, h->n, h->n_inst, d_theta, W, stride, h->d_ws, h->d_ws_ok, d_out);
+    EpochData d{h->d_t, h->d_vel, h->d_s2, h->d_inst, h->d_tab, h->t0, h->par};
+    h->launch(st, d, h->n, h->n_inst, d_theta, W, stride, d_out);
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

@@ -22,11 +22,11 @@
 //         ~K d^3, ~1e-6); at most 8 iterations.  The large early steps cost
 //         fp32 issue slots, not fp64 ones;
 //      3. sin/cos of the fp32 root in fp64 from an LDS table of sin/cos at
-//         j*pi/128 plus a degree-7/8 Taylor rotation (|d| <= pi/256);
+//         j*pi/32 plus a degree-7/8 Taylor rotation (|d| <= pi/64);
 //      4. Householder order-3 steps (quartic convergence) with sin/cos carried
-//         by short-series rotation, until the local error estimate
-//         (e/f')^3 d^4 < 1e-17: one step for a seed within ~1e-4 unless e is
-//         close to 1.
+//         by short-series rotation, until the local error bound
+//         (e/f')^3 d^4 < 1e-17: one step whenever the seed is within 1e-5 and
+//         e <= 0.9, which is the common case.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -100,6 +100,13 @@ __device__ __forceinline__ void sincos_f32(float x, float &s, float &c) {
     float cc = (q & 1) ? sn : cs;
     s = (q & 2) ? -ss : ss;
     c = ((q + 1) & 2) ? -cc : cc;
+}
+
+// 1/b with one Newton-Raphson step on v_rcp_f64 (~2^-50 relative): enough for a
+// summand such as r^2/s^2, whose rounding is below the reduction's own.
+__device__ __forceinline__ double rcp_nr1(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
 }
 
 // 1/b to ~1 ulp: v_rcp_f64 + two Newton-Raphson steps (finite, normal b).
@@ -207,9 +214,13 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
 #ifndef RVK_SEED_HW
 #define RVK_SEED_HW 1
 #endif
-    const float Ef = (!RVK_SEED_HW || ef > 0.95f) ? seed_f32<true>(rf, ef) : seed_f32<false>(rf, ef);
+#ifndef RVK_ABLATE
+#define RVK_ABLATE 0   // timing experiments only (wrong results): 1 = no fp64 stage, 2 = no fp32 seed, 3 = neither
+#endif
+    const float Ef = (RVK_ABLATE & 2) ? rf : ((!RVK_SEED_HW || ef > 0.95f) ? seed_f32<true>(rf, ef) : seed_f32<false>(rf, ef));
     double E = (double)Ef, S, C;
     sincos_tab(E, tab, S, C);
+    if (RVK_ABLATE & 1) { cosE = C; sinE = S; return; }
 #pragma unroll 1
     for (int it = 0; it < 8; ++it) {
         const double f = E - e * S - r;
@@ -226,21 +237,83 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
         const double ad = __builtin_fabs(d);
         if (ad > 1e-4) {                   // too far for the short series: re-anchor on the table
             sincos_tab(E, tab, S, C);
-        } else {
+        } else {                           // |d| <= 1e-4: sin d = d - d^3/6 (+8e-23), cos d = 1 - d^2/2 (+4e-18)
             const double z = d * d;
             const double sd = __builtin_fma(d * z, -1.0 / 6.0, d);
-            const double cm = z * __builtin_fma(z, 1.0 / 24.0, -0.5);
+            const double cm = -0.5 * z;
             const double Sn = __builtin_fma(S, cm, __builtin_fma(C, sd, S));
             const double Cn = __builtin_fma(C, cm, __builtin_fma(-S, sd, C));
             S = Sn;
             C = Cn;
         }
-        // next error ~ (e/f1)^3 d^4 ~ 6 e^3 d^4 / den
-        const double z2 = (d * d) * (d * d);
-        if (z2 * e6e3 * __builtin_fabs(t) < 1e-17) break;
+        // next error ~ (e/f1)^3 d^4.  For e <= 0.9, (e/f1)^3 <= 729, so |d| <= 1e-5 already
+        // bounds it by 7.3e-18 (one compare); otherwise estimate it as 6 e^3 d^4 / den.
+#ifndef RVK_HH_SINGLE
+#define RVK_HH_SINGLE 1
+#endif
+        if (RVK_HH_SINGLE && e <= 0.9) {
+            if (ad <= 1e-5) break;
+        } else {
+            const double z2 = (d * d) * (d * d);
+            if (z2 * e6e3 * __builtin_fabs(t) < 1e-17) break;
+        }
     }
     cosE = C;
     sinE = S;
+}
+
+// ---- register-light atan / atan2 / tan for the Tc and secosw/sesinw conversions ----
+// fdlibm's s_atan.c algorithm (< 1 ulp): argument reduction to |x| < 7/16 against
+// atan(0.5), atan(1), atan(1.5), atan(inf), then an 11-term odd polynomial.  Used by
+// the in-kernel conversion instead of OCML's atan/atan2/tan.
+__device__ __forceinline__ double atan_fd(double x) {
+    constexpr double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                     aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                     aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                     aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                     aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                     aT10 = 1.62858201153657823623e-02;
+    const double ax = __builtin_fabs(x);
+    // reduction: id = -1 (none), 0..3
+    double num, den, hi, lo;
+    int id;
+    if (ax < 0.4375) { id = -1; num = ax; den = 1.0; hi = 0.0; lo = 0.0; }
+    else if (ax < 0.6875) { id = 0; num = 2.0 * ax - 1.0; den = 2.0 + ax;
+                            hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+    else if (ax < 1.1875) { id = 1; num = ax - 1.0; den = ax + 1.0;
+                            hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+    else if (ax < 2.4375) { id = 2; num = ax - 1.5; den = 1.0 + 1.5 * ax;
+                            hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+    else { id = 3; num = -1.0; den = ax; hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+    const double xr = (id < 0) ? ax : num / den;
+    const double z = xr * xr, w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    double r;
+    if (id < 0) r = xr - xr * (s1 + s2);
+    else r = hi - ((xr * (s1 + s2) - lo) - xr);
+    if (!(ax == ax)) r = x;                   // NaN propagates
+    return __builtin_copysign(r, x);
+}
+
+// atan2 with C99 / numpy signed-zero semantics; atan2(+0, u < 0) == pi exactly
+// (ravest then rejects w == pi, param.py:80-86).
+__device__ __forceinline__ double atan2_fd(double y, double x) {
+    constexpr double pi_lo = 1.2246467991473531772e-16;
+    if (y == 0.0) {
+        const bool xneg = (x < 0.0) || (x == 0.0 && __builtin_signbit(x));
+        return xneg ? __builtin_copysign(kPi, y) : y;
+    }
+    if (x == 0.0) return __builtin_copysign(kPi / 2, y);
+    const double z = atan_fd(__builtin_fabs(y / x));
+    if (x > 0.0) return __builtin_copysign(z, y);
+    return __builtin_copysign(kPi - (z - pi_lo), y);
+}
+
+__device__ __forceinline__ double tan_fd(double x) {
+    double s, c;
+    sincos_mod(x, s, c);
+    return s / c;
 }
 
 // Per-planet constants in the default "P K e w Tp" form (model.py:199-206,
@@ -266,7 +339,7 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
     if (par >= 2) {                       // secosw/sesinw -> e, w  (param.py:217-234)
         double u = p5[2], v = p5[3];
         e = u * u + v * v;
-        w = atan2(v, u);
+        w = atan2_fd(v, u);
     } else {
         e = p5[2];
         w = p5[3];
@@ -278,8 +351,10 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
             Tp = 0.0;
         } else {
             double theta_tc = (kPi / 2) - w;
-            double E = 2 * atan(sqrt((1 - e) / (1 + e)) * tan(theta_tc / 2));
-            double Mc = E - (e * sin(E));
+            double E = 2 * atan_fd(sqrt((1 - e) / (1 + e)) * tan_fd(theta_tc / 2));
+            double sE, cE;
+            sincos_mod(E, sE, cE);
+            double Mc = E - (e * sE);
             Tp = p5[4] - (P / kTwoPi) * Mc;
         }
     } else {
@@ -302,7 +377,9 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
     return ok;
 }
 
-__device__ __forceinline__ bool planet_consts(int par, const double *p5, PlanetK &pk) {
+// Out of line on purpose: an inlined conversion (atan/tan/sqrt/division chains) would
+// set the whole kernel's VGPR budget; as a call it costs registers only while it runs.
+__device__ __attribute__((noinline)) bool planet_consts(int par, const double *p5, PlanetK &pk) {
     return planet_consts_t<-1>(p5, pk, par);
 }
 
