@@ -61,7 +61,8 @@ typedef struct rvk_handle rvk_handle;
 
 /* Create a handle bound to HIP device `device` (ordinal; -1 = current device).
  * Copies the data arrays to the device once (LogLikelihood precompute).
- * inst_idx may be NULL when n_inst == 1. Returns NULL on error. */
+ * inst_idx may be NULL when n_inst == 1.  n_epochs == 0 (NULL arrays) makes a
+ * model-only handle for rvk_predict*.  Returns NULL on error. */
 rvk_handle *rvk_create(const double *time, const double *vel, const double *velerr,
                        const int32_t *inst_idx, int32_t n_epochs, int32_t n_inst,
                        int32_t n_planets, int32_t parameterisation, double t0,
@@ -90,6 +91,12 @@ int rvk_reserve(rvk_handle *h, int64_t max_walkers);
  * Invalid planets give NaN rows. Host buffers, blocking. */
 int rvk_predict(rvk_handle *h, const double *theta, int64_t n_samples, int64_t row_stride,
                 const double *t, const int32_t *inst, int64_t n_t, uint32_t what, double *out);
+
+/* rvk_predict on device buffers, stream-ordered (d_inst may be NULL unless
+ * RVK_PRED_GAMMA with n_inst > 1).  d_out is [n_samples][n_t]. */
+int rvk_predict_device(rvk_handle *h, const double *d_theta, int64_t n_samples, int64_t row_stride,
+                       const double *d_t, const int32_t *d_inst, int64_t n_t, uint32_t what,
+                       double *d_out, void *stream);
 
 /* Kepler solve on the device for arrays (host buffers): cos E, sin E of
  * E - e sin E = M.  solver 0: production solver (fp32 seed + fp64 Halley

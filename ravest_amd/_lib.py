@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "librvk.so")
 LIB_PATH = os.environ.get("RAVEST_AMD_LIB", LIB_PATH)
 
 # every symbol declared in include/rvk.h
-EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rvk_reserve", "rvk_predict",
+EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rvk_reserve", "rvk_predict", "rvk_predict_device",
            "rvk_solve_kepler", "rvk_set_option", "rvk_stream", "rvk_sync", "rvk_device_count",
            "rvk_last_error", "rvk_version"]
 
@@ -54,6 +54,7 @@ def load() -> C.CDLL:
     L.rvk_loglike.argtypes = [vp, dp, C.c_int64, C.c_int64, dp]
     L.rvk_loglike_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
     L.rvk_predict.argtypes = [vp, dp, C.c_int64, C.c_int64, dp, ip, C.c_int64, C.c_uint32, dp]
+    L.rvk_predict_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp, C.c_int64, C.c_uint32, vp, vp]
     L.rvk_solve_kepler.argtypes = [dp, dp, C.c_int64, dp, dp, C.c_int32, C.c_int32]
     L.rvk_set_option.argtypes = [vp, C.c_int32, C.c_int32]
     L.rvk_reserve.argtypes = [vp, C.c_int64]
@@ -63,7 +64,7 @@ def load() -> C.CDLL:
     L.rvk_device_count.argtypes = []
     L.rvk_last_error.restype = C.c_char_p
     L.rvk_version.restype = C.c_int
-    for name in ("rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_solve_kepler", "rvk_sync",
+    for name in ("rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
                  "rvk_set_option", "rvk_reserve"):
         getattr(L, name).restype = C.c_int
     _lib = L

@@ -381,13 +381,14 @@ static void free_handle(rvk_handle *h) {
 static int create_impl(rvk_handle *h, const double *time, const double *vel, const double *velerr,
                        const int32_t *inst_idx, int32_t n, int32_t n_inst, int32_t n_planets, int32_t par,
                        double t0, int32_t device) {
-    if (n < 1 || !time || !vel || !velerr) return fail(RVK_E_ARG, "n_epochs must be >= 1 with non-NULL data");
+    if (n < 0 || (n > 0 && (!time || !vel || !velerr)))
+        return fail(RVK_E_ARG, "n_epochs must be >= 0 with non-NULL data (0 = model-only handle for rvk_predict)");
     if (n_planets < 1 || n_planets > RVK_MAX_PLANETS) return fail(RVK_E_ARG, "n_planets must be in [1, 8]");
     if (n_inst < 1 || n_inst > RVK_MAX_INST) return fail(RVK_E_ARG, "n_inst must be in [1, 16]");
     if (par < 0 || par > 3) return fail(RVK_E_ARG, "unknown parameterisation code");
-    if (n_inst > 1 && !inst_idx) return fail(RVK_E_ARG, "inst_idx is required when n_inst > 1");
-    std::vector<int32_t> inst(n, 0);
-    if (inst_idx)
+    if (n > 0 && n_inst > 1 && !inst_idx) return fail(RVK_E_ARG, "inst_idx is required when n_inst > 1");
+    std::vector<int32_t> inst((size_t)n, 0);
+    if (inst_idx && n > 0)
         for (int i = 0; i < n; ++i) {
             if (inst_idx[i] < 0 || inst_idx[i] >= n_inst) return fail(RVK_E_ARG, "inst_idx out of range");
             inst[i] = inst_idx[i];
@@ -407,6 +408,8 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->launch = pick_ll(n_planets, n_inst > 1, 0, par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    if ((rc = upload_table(&h->d_tab))) return rc;
+    if (n == 0) return RVK_OK;                                      // model-only handle
     std::vector<double> s2(n);
     for (int i = 0; i < n; ++i) s2[i] = velerr[i] * velerr[i];     // velerr ** 2 (fit.py:3598)
     size_t bd = sizeof(double) * (size_t)n;
@@ -415,7 +418,6 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     HIPCHK(hipMalloc(&h->d_s2, bd));
     HIPCHK(hipMalloc(&h->d_inst, sizeof(int32_t) * (size_t)n));
     HIPCHK(hipMemcpy(h->d_t, time, bd, hipMemcpyHostToDevice));
-    if ((rc = upload_table(&h->d_tab))) return rc;
     HIPCHK(hipMemcpy(h->d_vel, vel, bd, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_s2, s2.data(), bd, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_inst, inst.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice));
@@ -461,6 +463,7 @@ int rvk_sync(rvk_handle *h) {
 
 static int check_rows(rvk_handle *h, int64_t W, int64_t stride) {
     if (!h) return fail(RVK_E_ARG, "NULL handle");
+    if (W < 0) return fail(RVK_E_ARG, "negative row count");
     if (W < 0) return fail(RVK_E_ARG, "n_walkers < 0");
     long long pfull = 5LL * h->n_planets + 2LL * h->n_inst + 2;
     if (stride < pfull) return fail(RVK_E_ARG, "row_stride < P_full = 5*n_planets + 2*n_inst + 2");
@@ -478,6 +481,7 @@ int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t W, int64_t 
                        void *stream) {
     int rc = check_rows(h, W, stride);
     if (rc) return rc;
+    if (h->n < 1) return fail(RVK_E_ARG, "model-only handle (n_epochs = 0) has no data to evaluate");
     if (W == 0) return RVK_OK;
     if (!d_theta || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     hipStream_t st = (hipStream_t)stream;   // used as given: NULL is HIP's default stream
@@ -504,6 +508,39 @@ int rvk_loglike(rvk_handle *h, const double *theta, int64_t W, int64_t stride, d
     return RVK_OK;
 }
 
+int rvk_predict_device(rvk_handle *h, const double *d_theta, int64_t S, int64_t stride, const double *d_t,
+                       const int32_t *d_inst, int64_t n_t, uint32_t what, double *d_out, void *stream) {
+    int rc = check_rows(h, S, stride);
+    if (rc) return rc;
+    if (S == 0 || n_t == 0) return RVK_OK;
+    if (!d_theta || !d_t || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
+    if ((what & RVK_PRED_GAMMA) && h->n_inst > 1 && !d_inst) return fail(RVK_E_ARG, "inst required for GAMMA");
+    unsigned planets = what & RVK_PRED_PLANETS & ((1u << h->n_planets) - 1u);
+    const int nsel = __builtin_popcount(planets);
+    what = (what & ~RVK_PRED_PLANETS) | planets;
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    dim3 grid = wave_grid(S);
+#define PRED_CASE(K)                                                                                           \
+    case K:                                                                                                    \
+        if (h->solver == 1)                                                                                    \
+            hipLaunchKernelGGL((predict_kernel<K, 1>), grid, dim3(kBlock), 0, st, d_t, d_inst, (long long)n_t,  \
+                               h->n_planets, h->n_inst, h->par, h->t0, d_theta, (long long)S, (long long)stride,\
+                               what, h->d_tab, d_out);                                                         \
+        else                                                                                                   \
+            hipLaunchKernelGGL((predict_kernel<K, 0>), grid, dim3(kBlock), 0, st, d_t, d_inst, (long long)n_t,  \
+                               h->n_planets, h->n_inst, h->par, h->t0, d_theta, (long long)S, (long long)stride,\
+                               what, h->d_tab, d_out);                                                         \
+        break;
+    switch (nsel) {
+        PRED_CASE(0) PRED_CASE(1) PRED_CASE(2) PRED_CASE(3) PRED_CASE(4) PRED_CASE(5) PRED_CASE(6)
+        PRED_CASE(7) PRED_CASE(8)
+    }
+#undef PRED_CASE
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
 int rvk_predict(rvk_handle *h, const double *theta, int64_t S, int64_t stride, const double *t,
                 const int32_t *inst, int64_t n_t, uint32_t what, double *out) {
     int rc = check_rows(h, S, stride);
@@ -511,48 +548,35 @@ int rvk_predict(rvk_handle *h, const double *theta, int64_t S, int64_t stride, c
     if (S == 0 || n_t == 0) return RVK_OK;
     if (!theta || !t || !out) return fail(RVK_E_ARG, "NULL host buffer");
     if ((what & RVK_PRED_GAMMA) && h->n_inst > 1 && !inst) return fail(RVK_E_ARG, "inst required for GAMMA");
-    unsigned planets = what & RVK_PRED_PLANETS & ((1u << h->n_planets) - 1u);
-    int nsel = __builtin_popcount(planets);
-    what = (what & ~RVK_PRED_PLANETS) | planets;
     HIPCHK(hipSetDevice(h->device));
+    // samples in chunks so the device output block stays <= 2^25 doubles (256 MB)
+    long long chunk = (1LL << 25) / n_t;
+    if (chunk < 1) chunk = 1;
+    if (chunk > S) chunk = S;
     double *d_th = nullptr, *d_t = nullptr, *d_o = nullptr;
     int32_t *d_i = nullptr;
-    size_t bt = sizeof(double) * (size_t)S * (size_t)stride;
-    HIPCHK(hipMalloc(&d_th, bt));
+    HIPCHK(hipMalloc(&d_th, sizeof(double) * (size_t)chunk * (size_t)stride));
     HIPCHK(hipMalloc(&d_t, sizeof(double) * n_t));
-    HIPCHK(hipMalloc(&d_o, sizeof(double) * S * n_t));
+    HIPCHK(hipMalloc(&d_o, sizeof(double) * (size_t)chunk * (size_t)n_t));
     if (inst) {
         HIPCHK(hipMalloc(&d_i, sizeof(int32_t) * n_t));
         HIPCHK(hipMemcpyAsync(d_i, inst, sizeof(int32_t) * n_t, hipMemcpyHostToDevice, h->stream));
     }
-    HIPCHK(hipMemcpyAsync(d_th, theta, bt, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(d_t, t, sizeof(double) * n_t, hipMemcpyHostToDevice, h->stream));
-    dim3 grid = wave_grid(S);
-#define PRED_CASE(K)                                                                                        \
-    case K:                                                                                                 \
-        if (h->solver == 1)                                                                                 \
-            hipLaunchKernelGGL((predict_kernel<K, 1>), grid, dim3(kBlock), 0, h->stream, d_t, d_i,           \
-                               (long long)n_t, h->n_planets, h->n_inst, h->par, h->t0, d_th, (long long)S,  \
-                               (long long)stride, what, h->d_tab, d_o);                                     \
-        else                                                                                                \
-            hipLaunchKernelGGL((predict_kernel<K, 0>), grid, dim3(kBlock), 0, h->stream, d_t, d_i,           \
-                               (long long)n_t, h->n_planets, h->n_inst, h->par, h->t0, d_th, (long long)S,  \
-                               (long long)stride, what, h->d_tab, d_o);                                     \
-        break;
-    switch (nsel) {
-        PRED_CASE(0) PRED_CASE(1) PRED_CASE(2) PRED_CASE(3) PRED_CASE(4) PRED_CASE(5) PRED_CASE(6)
-        PRED_CASE(7) PRED_CASE(8)
+    for (long long s0 = 0; s0 < S && rc == RVK_OK; s0 += chunk) {
+        const long long ns = (S - s0) < chunk ? (S - s0) : chunk;
+        HIPCHK(hipMemcpyAsync(d_th, theta + s0 * stride, sizeof(double) * ns * stride, hipMemcpyHostToDevice,
+                              h->stream));
+        rc = rvk_predict_device(h, d_th, ns, stride, d_t, d_i, n_t, what, d_o, h->stream);
+        if (rc == RVK_OK)
+            HIPCHK(hipMemcpyAsync(out + s0 * n_t, d_o, sizeof(double) * ns * n_t, hipMemcpyDeviceToHost, h->stream));
     }
-#undef PRED_CASE
-    hipError_t le = hipGetLastError();
-    HIPCHK(hipMemcpyAsync(out, d_o, sizeof(double) * S * n_t, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     (void)hipFree(d_th);
     (void)hipFree(d_t);
     (void)hipFree(d_o);
     (void)hipFree(d_i);
-    if (le != hipSuccess) return fail(RVK_E_HIP, std::string("predict_kernel: ") + hipGetErrorString(le));
-    return RVK_OK;
+    return rc;
 }
 
 int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, double *sinE, int32_t device,

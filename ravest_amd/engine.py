@@ -30,9 +30,10 @@ class RVEngine:
         if isinstance(parameterisation, str):
             parameterisation = Parameterisation(parameterisation)
         self.parameterisation = parameterisation
-        self.time = np.ascontiguousarray(time, np.float64)
-        self.vel = np.ascontiguousarray(vel, np.float64)
-        self.velerr = np.ascontiguousarray(velerr, np.float64)
+        model_only = time is None                     # rvk_predict only (n_epochs = 0)
+        self.time = np.zeros(0) if model_only else np.ascontiguousarray(time, np.float64)
+        self.vel = np.zeros(0) if model_only else np.ascontiguousarray(vel, np.float64)
+        self.velerr = np.zeros(0) if model_only else np.ascontiguousarray(velerr, np.float64)
         n = self.time.size
         if not (self.vel.size == n and self.velerr.size == n):
             raise ValueError("time, vel and velerr must have the same length")
@@ -40,7 +41,10 @@ class RVEngine:
                          else np.ascontiguousarray(inst_idx, np.int32))
         self.n_epochs, self.n_inst, self.n_planets, self.t0 = n, int(n_inst), int(n_planets), float(t0)
         self.p_full = 5 * self.n_planets + 2 * self.n_inst + 2
-        self._h = L.rvk_create(_p(self.time), _p(self.vel), _p(self.velerr), _p(self.inst_idx, _ip),
+        nul = C.POINTER(C.c_double)()
+        self._h = L.rvk_create(nul if model_only else _p(self.time), nul if model_only else _p(self.vel),
+                               nul if model_only else _p(self.velerr),
+                               C.POINTER(C.c_int32)() if model_only else _p(self.inst_idx, _ip),
                                n, self.n_inst, self.n_planets, parameterisation.code, self.t0, int(device))
         if not self._h:
             raise _lib.RVKError(f"rvk_create failed: {_lib.last_error()}")
@@ -65,10 +69,7 @@ class RVEngine:
         _lib.check(_lib.load().rvk_loglike_device(self._h, theta.data_ptr(), theta.shape[0], theta.stride(0),
                                                   out.data_ptr(), stream.cuda_stream))
 
-    def predict(self, theta: np.ndarray, t, inst=None, planets=None, trend=True, gamma=False) -> np.ndarray:
-        """Posterior-predictive RV [S, T] (sum of the selected planets [+ trend] [+ gamma])."""
-        theta = np.ascontiguousarray(np.atleast_2d(theta), np.float64)
-        t = np.ascontiguousarray(t, np.float64)
+    def _what(self, planets, trend, gamma) -> int:
         planets = range(self.n_planets) if planets is None else planets
         what = 0
         for p in planets:
@@ -77,6 +78,23 @@ class RVEngine:
             what |= _lib.PRED_TREND
         if gamma:
             what |= _lib.PRED_GAMMA
+        return what
+
+    def predict_device(self, theta, t, out, inst=None, planets=None, trend=True, gamma=False, stream=None) -> None:
+        """Device form of :meth:`predict` on torch tensors (theta [S, >=P_full], t [T], out [S, T])."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(theta.device)
+        _lib.check(_lib.load().rvk_predict_device(self._h, theta.data_ptr(), theta.shape[0], theta.stride(0),
+                                                  t.data_ptr(), 0 if inst is None else inst.data_ptr(), t.numel(),
+                                                  self._what(planets, trend, gamma), out.data_ptr(),
+                                                  stream.cuda_stream))
+
+    def predict(self, theta: np.ndarray, t, inst=None, planets=None, trend=True, gamma=False) -> np.ndarray:
+        """Posterior-predictive RV [S, T] (sum of the selected planets [+ trend] [+ gamma])."""
+        theta = np.ascontiguousarray(np.atleast_2d(theta), np.float64)
+        t = np.ascontiguousarray(t, np.float64)
+        what = self._what(planets, trend, gamma)
         ip = None
         if inst is not None:
             inst = np.ascontiguousarray(inst, np.int32)

@@ -149,3 +149,37 @@ def test_large_batch_mask_and_determinism():
     # 2 % of the ball is broken: e >= 1 and K <= 0 rows are -inf here; jit < 0 rows are
     # rejected by LogPosterior (fit.py:3465-3468), not by the likelihood
     assert (~np.isfinite(a)).sum() >= int(0.02 * len(a) * 2 / 3) - 2
+
+
+@pytest.mark.parametrize("np_,ni,par", [(5, 4, "P K e w Tc"), (8, 3, "P K secosw sesinw Tp"), (4, 1, "P K e w Tp")])
+def test_many_planets_and_instruments_vs_oracle(np_, ni, par):
+    from oracle import oracle
+    from ravest_amd.engine import RVEngine
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(np_, 300, ni, seed=100 + np_, parameterisation=par, trend=True)
+    th = make_walkers(ds, 517, seed=100 + np_)             # W not a multiple of 4
+    eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation, ds.t0)
+    ll = eng.loglike(th)
+    ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation.code, ds.t0, th)
+    assert_ll_close(ll, ref, what=f"np{np_}-ni{ni}")
+
+
+def test_hostile_inputs_do_not_fault():
+    """NaN / inf / huge parameters: bounded loops, clamped table index, -inf or NaN like the reference."""
+    from oracle import oracle
+    from ravest_amd.engine import RVEngine
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(2, 130, 1, seed=5)
+    th = make_walkers(ds, 64, seed=5, frac_invalid=0.0)
+    bad = [np.nan, np.inf, -np.inf, 1e300, -1e300, 1e-300, 0.0]
+    rng = np.random.default_rng(0)
+    for r in range(len(th)):
+        if r % 2:
+            th[r, rng.integers(th.shape[1])] = bad[r % len(bad)]
+    eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 2, ds.parameterisation, ds.t0)
+    ll = eng.loglike(th)
+    ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 2, 0, ds.t0, th)
+    assert np.array_equal(np.isneginf(ll), np.isneginf(ref))
+    fin = np.isfinite(ref) & np.isfinite(ll)
+    assert np.all(np.abs(ll[fin] - ref[fin]) <= 1e-9 * np.maximum(1, np.abs(ref[fin])))
+    assert np.array_equal(np.isfinite(ll), np.isfinite(ref))

@@ -1,0 +1,102 @@
+"""Posterior predictive: rvk_predict vs the reference's Planet/Trend (golden)
+and the C oracle."""
+import numpy as np
+import pytest
+
+from tests._golden import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _pp(ds, free):
+    from ravest_amd.predictive import PosteriorPredictive
+    fixed = {n: ds.truth[n] for n in ds.names if n not in free}
+    return PosteriorPredictive(ds.planet_letters, ds.parameterisation, fixed, free, ds.unique_instruments, ds.t0)
+
+
+def _oracle_total(ds, full, times):
+    from oracle import oracle
+    code = ds.parameterisation.code
+    out = np.zeros((len(full), len(times)))
+    np_ = len(ds.planet_letters)
+    ni = len(ds.unique_instruments)
+    for s, row in enumerate(full):
+        gd, gdd = row[5 * np_ + 2 * ni], row[5 * np_ + 2 * ni + 1]
+        dt = times - ds.t0
+        tot = (0.0 + (gd * dt if gd != 0 else 0.0)) + (gdd * (dt * dt) if gdd != 0 else 0.0)
+        for p in range(np_):
+            tot = tot + oracle.planet_rv(code, row[5 * p:5 * p + 5], times)
+        out[s] = tot
+    return out
+
+
+@pytest.mark.parametrize("par", ["P K e w Tp", "P K secosw sesinw Tc"])
+def test_total_from_samples_vs_oracle(par):
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(3, 64, 2, seed=7, parameterisation=par, trend=True)
+    th = make_walkers(ds, 300, seed=7, frac_invalid=0.0)
+    free = [n for n in ds.names if not n.startswith(("g_", "jit_"))]
+    pp = _pp(ds, free)
+    times = np.concatenate([np.linspace(0, 1000, 400), np.linspace(2.0e3, 2.5e3, 50)])
+    samples = th[:, [ds.names.index(n) for n in free]]
+    got = pp.rv_total_from_samples(times, samples)
+    ref = _oracle_total(ds, pp.full(samples), times)
+    K = sum(ds.truth[f"K_{L}"] for L in ds.planet_letters)
+    assert np.max(np.abs(got - ref)) <= 1e-9 * K
+    trend = pp.rv_trend_from_samples(times, samples)
+    pb = pp.rv_planet_from_samples("b", times, samples)
+    assert got.shape == trend.shape == pb.shape == (300, len(times))
+    parts = trend + sum(pp.rv_planet_from_samples(L, times, samples) for L in ds.planet_letters)
+    assert np.max(np.abs(parts - got)) <= 1e-10 * K
+
+
+def test_custom_vs_reference_planet_golden():
+    """calculate_rv_planet_custom == Planet(...).radial_velocity (golden from the reference)."""
+    from ravest_amd.param import Parameterisation
+    from ravest_amd.predictive import PosteriorPredictive
+    g = np.load(f"{GOLDEN}/planet_rv.npz")
+    for code, par in enumerate(["P K e w Tp", "P K e w Tc", "P K secosw sesinw Tp", "P K secosw sesinw Tc"]):
+        P_ = Parameterisation(par)
+        pp = PosteriorPredictive(["b"], P_, {}, [], ["HARPS"], 0.0)
+        t, prm, ref = g[f"t_{code}"], g[f"params_{code}"], g[f"rv_{code}"]
+        for p5, r in zip(prm, ref):
+            params = {f"{k}_b": v for k, v in zip(P_.pars, p5)} | {"g_HARPS": 0, "jit_HARPS": 0, "gd": 0, "gdd": 0}
+            if np.isnan(r).all():
+                with pytest.raises(ValueError):
+                    pp.rv_planet_custom("b", t, params)
+                continue
+            got = pp.rv_planet_custom("b", t, params)
+            Mabs = (2 * np.pi / p5[0]) * np.abs(t + 2.5e6)
+            assert np.all(np.abs(got - r) <= 1e-10 * abs(p5[1]) + 4e-16 * Mabs * abs(p5[1]) / 0.03)
+
+
+def test_invalid_sample_raises():
+    from ravest_amd.synth import make_dataset
+    ds = make_dataset(1, 16, 1, seed=3)
+    pp = _pp(ds, ["K_b"])
+    with pytest.raises(ValueError):
+        pp.rv_planet_from_samples("b", np.linspace(0, 10, 5), np.array([[5.0], [-1.0]]))
+
+
+def test_large_grid_device_path_and_rate():
+    import time
+    import torch
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(2, 16, 1, seed=9)
+    th = make_walkers(ds, 20000, seed=9, frac_invalid=0.0)
+    pp = _pp(ds, list(ds.names))
+    times = np.linspace(0, 1000, 1000)
+    host = pp.engine.predict(th, times)
+    d_th = torch.from_numpy(th).cuda()
+    d_t = torch.from_numpy(times).cuda()
+    out = torch.empty((len(th), len(times)), dtype=torch.float64, device="cuda")
+    pp.engine.predict_device(d_th, d_t, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), host)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        pp.engine.predict_device(d_th, d_t, out)
+    torch.cuda.synchronize()
+    rate = 5 * th.shape[0] * len(times) * 2 / (time.perf_counter() - t0)
+    print(f"predictive: {rate:.3e} Kepler solves/s")
+    assert rate > 1e10
