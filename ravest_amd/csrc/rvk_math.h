@@ -46,8 +46,12 @@ constexpr double kPio2Lo  = -1.4973849048591698e-33;
 constexpr double kLn2     = 0.6931471805599453;
 constexpr double kLog2Pi  = 1.8378770664093453;       // == np.log(2*np.pi)
 
-// Reduce x by 2*pi: r = x - k*2*pi, |r| <= pi (+ulp), abs error ~1e-15 for any |x| < 1e15.
+// Reduce x by 2*pi: r = x - k*2*pi, |r| <= pi (+ulp), abs error ~1e-15 for |x| < 2^50.
+// Beyond 2^50 rad (ulp(M) > 2^-3: no phase information left; e.g. P = 1 d with
+// |t - Tp| > 1.8e14 d) the result is defined as 0: finite, unspecified physically
+// (the reference returns equally meaningless finite values there).
 __device__ __forceinline__ double reduce_2pi(double x) {
+    x = (__builtin_fabs(x) >= 0x1p50 && __builtin_fabs(x) < __builtin_inf()) ? 0.0 : x;   // NaN, inf propagate
     double k = __builtin_rint(x * kInv2Pi);
     double r = __builtin_fma(-k, k2PiHi, x);
     r = __builtin_fma(-k, k2PiMi, r);
@@ -106,7 +110,8 @@ __device__ __forceinline__ void sincos_f32(float x, float &s, float &c) {
 // summand such as r^2/s^2, whose rounding is below the reduction's own.
 __device__ __forceinline__ double rcp_nr1(double b) {
     double r = __builtin_amdgcn_rcp(b);
-    return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+    // fmin drops the NaN that -inf * 0 makes for b = inf, so 1/inf = 0 as in IEEE division
+    return __builtin_fma(r, __builtin_fmin(__builtin_fma(-b, r, 1.0), 1.0), r);
 }
 
 // 1/b to ~1 ulp: v_rcp_f64 + two Newton-Raphson steps (finite, normal b).
@@ -318,10 +323,11 @@ __device__ __forceinline__ double tan_fd(double x) {
 
 // Per-planet constants in the default "P K e w Tp" form (model.py:199-206,
 // model.py:302 n = 2*pi/P).  ok == false exactly where Planet() raises.
-// rv = inv * ((cosE - e) * Kcw - sinE * Ksqsw) + Kecw,  inv = 1 / (1 - e cosE)
-// (= K (cos f cos w - sin f sin w + e cos w), model.py:119-121,170)
+// rv = K * (inv * ((cosE - e) * cw - sinE * sqsw) + ecw),  inv = 1 / (1 - e cosE)
+// (= K (cos f cos w - sin f sin w + e cos w), model.py:119-121,170; K stays the
+// outer factor so K = inf gives +-inf like the reference, not inf - inf)
 struct PlanetK {
-    double n, Tp, e, Kcw, Ksqsw, Kecw, e6e3, pad;
+    double n, Tp, e, K, cw, sqsw, ecw, e6e3;
 };
 
 // param.py:88-105 (NaN passes the '<=' tests, as in the reference)
@@ -369,11 +375,11 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
     pk.e = e;
     double sw, cw;
     sincos_mod(w, sw, cw);
-    pk.Kcw = K * cw;
-    pk.Ksqsw = K * sqrt(1.0 - e * e) * sw;
-    pk.Kecw = K * (e * cw);
+    pk.K = K;
+    pk.cw = cw;
+    pk.sqsw = sqrt(1.0 - e * e) * sw;
+    pk.ecw = e * cw;
     pk.e6e3 = 6.0 * e * e * e;
-    pk.pad = 0.0;
     return ok;
 }
 
@@ -392,7 +398,7 @@ __device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const S
     if (SOLVER == 1) solve_kepler_ref(M, pk.e, cE, sE);
     else solve_kepler_fast(M, pk.e, pk.e6e3, tab, cE, sE);
     const double inv = rcp_nr(1.0 - pk.e * cE);
-    return __builtin_fma(inv, __builtin_fma(cE - pk.e, pk.Kcw, -sE * pk.Ksqsw), pk.Kecw);
+    return pk.K * __builtin_fma(inv, __builtin_fma(cE - pk.e, pk.cw, -sE * pk.sqsw), pk.ecw);
 }
 
 // Wave64 sum in a fixed order (bitwise reproducible): DPP butterflies inside each
