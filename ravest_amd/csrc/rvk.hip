@@ -128,6 +128,9 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             const double *jit = g + n_inst;
             const double gd = jit[n_inst], gdd = jit[n_inst + 1];
             const double g0 = g[0], j0 = jit[0] * jit[0];
+            PlanetK pk[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pk[p] = uniform_pk(pks[j][p]);
             double chi2 = 0.0, prod = 1.0;
             int expo = 0;
             // software pipeline: the next epoch's data is in flight during this epoch's solve
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                 }
                 double rv = 0.0;
 #pragma unroll
-                for (int p = 0; p < NP; ++p) rv += planet_rv<SOLVER>(pks[j][p], t, tab);
+                for (int p = 0; p < NP; ++p) rv += planet_rv<SOLVER>(pk[p], t, tab);
                 const double dt = t - d.t0;
                 rv += __builtin_fma(gd, dt, gdd * (dt * dt));
                 double gam = g0, jj = j0;

@@ -419,6 +419,23 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+__device__ __forceinline__ double uniform_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// A wave-uniform PlanetK (read from LDS with a uniform address) moved to SGPRs:
+// the 8 constants stay out of the VGPR budget of the epoch loop.
+__device__ __forceinline__ PlanetK uniform_pk(const PlanetK &q) {
+    PlanetK pk;
+    pk.n = uniform_d(q.n); pk.Tp = uniform_d(q.Tp); pk.e = uniform_d(q.e); pk.K = uniform_d(q.K);
+    pk.cw = uniform_d(q.cw); pk.sqsw = uniform_d(q.sqsw); pk.ecw = uniform_d(q.ecw);
+    pk.e6e3 = uniform_d(q.e6e3);
+    return pk;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
     v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
     v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]

@@ -33,6 +33,8 @@ def main():
     cases.append(("cfg2-Tc", ds))
     ds = make_dataset(2, 512, 1, seed=4, parameterisation="P K secosw sesinw Tc"); ds.theta = make_walkers(ds, 8192, seed=4)
     cases.append(("cfg4-secosw-Tc", ds))
+    ds = make_dataset(3, 256, 2, seed=6); ds.theta = make_walkers(ds, 4096, seed=6)
+    cases.append(("np3-2inst", ds))
     for name, ds in cases:
         eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), len(ds.planet_letters),
                        ds.parameterisation, ds.t0, device=0)
