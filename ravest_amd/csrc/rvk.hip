@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rvk.h"
@@ -131,45 +132,57 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             PlanetK pk[NP];
 #pragma unroll
             for (int p = 0; p < NP; ++p) pk[p] = uniform_pk(pks[j][p]);
-            double chi2 = 0.0, prod = 1.0;
-            int expo = 0;
-            // software pipeline: the next epoch's data is in flight during this epoch's solve
-            int i = lane;
-            double tn = t_1, vn = v_1, sn = s_1;
-            int in_ = i_1;
-            for (; i < n_epochs; i += 64) {
-                const double t = tn, vel = vn, s2b = sn;
-                const int ii = in_;
-                const int inx = i + 64;
-                if (inx < n_epochs) {
-                    tn = d.t[inx]; vn = d.vel[inx]; sn = d.s2[inx];
-                    if (MULTI) in_ = d.inst[inx];
-                }
-                double rv = 0.0;
-#pragma unroll
-                for (int p = 0; p < NP; ++p) rv += planet_rv<SOLVER>(pk[p], t, tab);
-                const double dt = t - d.t0;
-                rv += __builtin_fma(gd, dt, gdd * (dt * dt));
-                double gam = g0, jj = j0;
-                if (MULTI) {
-                    for (int k = 1; k < n_inst; ++k) {
-                        if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
+            double chi2 = 0.0, prod = 0.5;   // prod * 2^expo = running product of s^2
+            int expo = 1;
+            // The epoch loop, versioned on the (wave-uniform) trend so the trend-free
+            // common case carries no trend arithmetic at all.
+            auto epochs = [&](auto trend_c) {
+                constexpr bool TREND = decltype(trend_c)::value;
+                // software pipeline: the next epoch's data is in flight during this epoch's solve
+                double tn = t_1, vn = v_1, sn = s_1;
+                int in_ = i_1;
+                for (int i = lane; i < n_epochs; i += 64) {
+                    const double t = tn, vel = vn, s2b = sn;
+                    const int ii = in_;
+                    const int inx = i + 64;
+                    if (inx < n_epochs) {
+                        tn = d.t[inx]; vn = d.vel[inx]; sn = d.s2[inx];
+                        if (MULTI) in_ = d.inst[inx];
                     }
-                }
-                rv += gam;
-                const double s2 = s2b + jj;
-                const double r = rv - vel;
+                    double rv = 0.0;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) rv += planet_rv<SOLVER>(pk[p], t, tab);
+                    if (TREND) {
+                        const double dt = t - d.t0;
+                        rv += __builtin_fma(gd, dt, gdd * (dt * dt));
+                    }
+                    double gam = g0, jj = j0;
+                    if (MULTI) {
+                        for (int k = 1; k < n_inst; ++k) {
+                            if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
+                        }
+                    }
+                    rv += gam;
+                    const double s2 = s2b + jj;
+                    const double r = rv - vel;
 #if RVK_CHI_NR2
-                chi2 = __builtin_fma(r * r, rcp_nr(s2), chi2);
+                    chi2 = __builtin_fma(r * r, rcp_nr(s2), chi2);
 #else
-                chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);   // <= 2.2e-15 relative per term
+                    chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);   // <= 2.2e-15 relative per term
 #endif
-                prod *= s2;
-                int ex;
-                prod = __builtin_frexp(prod, &ex);
-                expo += ex;
+                    prod *= s2;
+                    int ex;
+                    prod = __builtin_frexp(prod, &ex);
+                    expo += ex;
+                }
+            };
+            if ((gd != 0.0) | (gdd != 0.0)) epochs(std::true_type{});
+            else epochs(std::false_type{});
+            double lsum = log_frexp(prod, expo);
+            const bool special = !(prod >= 0.5 && prod < 1.0);   // a product of 0, inf or NaN
+            if (__builtin_amdgcn_ballot_w64(special)) {          // rare: keep the generic log off the common path
+                if (special) lsum = log(prod) + (double)expo * kLn2;
             }
-            double lsum = log(prod) + (double)expo * kLn2;
             double tot = wave_sum(chi2 + lsum);
             if (lane == 0) out[w] = -0.5 * (tot + (double)n_epochs * kLog2Pi);
         }

@@ -157,6 +157,15 @@ constexpr double kTabInvH = 10.185916357881302;  // == 32 / np.pi
 
 struct SC { double s, c; };
 
+// a * b + c as one VOP3 v_fma_f64 with the constant c in SGPRs.  A Horner step
+// fma(z, p, c) otherwise comes out as the two-address v_fmac_f64, which needs c
+// copied into the destination first (an extra v_mov_b64 per coefficient).
+__device__ __forceinline__ double fma_s(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
 __device__ __forceinline__ void sincos_tab(double E, const SC *tab, double &S, double &C) {
     double jj = __builtin_rint(E * kTabInvH);
     jj = __builtin_fmin(__builtin_fmax(jj, (double)-kTabHalf), (double)kTabHalf);
@@ -164,8 +173,8 @@ __device__ __forceinline__ void sincos_tab(double E, const SC *tab, double &S, d
     const double d = E - a;                      // exact (Sterbenz)
     const SC sc = tab[(int)jj + kTabHalf];
     const double z = d * d;
-    const double sd = __builtin_fma(d * z, __builtin_fma(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
-    const double cm = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
+    const double sd = __builtin_fma(d * z, fma_s(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
+    const double cm = z * __builtin_fma(z, fma_s(z, __builtin_fma(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
     S = __builtin_fma(sc.s, cm, __builtin_fma(sc.c, sd, sc.s));
     C = __builtin_fma(sc.c, cm, __builtin_fma(-sc.s, sd, sc.c));
 }
@@ -417,6 +426,30 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)b, lane);
     const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// ln(m * 2^k) for a frexp mantissa m in [0.5, 1): fdlibm e_log.c's reduction and
+// kernel (m -> [sqrt(1/2), sqrt(2)), s = f / (2 + f), degree-14 polynomial in s),
+// ~1 ulp, about a quarter of the generic log's instructions.  Callers route
+// m outside [0.5, 1) (0, inf, NaN) to log().
+__device__ __forceinline__ double log_frexp(double m, int k) {
+    constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                     Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                     Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                     Lg7 = 1.479819860511658591e-01;
+    constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? 2.0 * m : m;
+    k -= lo ? 1 : 0;
+    const double f = m - 1.0;
+    const double hfsq = 0.5 * f * f;
+    const double s = f * rcp_nr(2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * fma_s(w, __builtin_fma(w, Lg6, Lg4), Lg2);
+    const double t2 = z * fma_s(w, fma_s(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
+    const double R = t2 + t1;
+    const double dk = (double)k;
+    return dk * ln2_hi - ((hfsq - __builtin_fma(s, hfsq + R, dk * ln2_lo)) - f);
 }
 
 __device__ __forceinline__ double uniform_d(double v) {
