@@ -15,15 +15,30 @@ LIB_PATH = os.path.join(_HERE, "lib", "librvk.so")
 # experiment hook: A/B builds of the same source (tools/variants.sh); never set in production
 LIB_PATH = os.environ.get("RAVEST_AMD_LIB", LIB_PATH)
 
-# every symbol declared in include/rvk.h
+# every symbol declared in include/rvk.h and include/rvk_post.h
 EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rvk_reserve", "rvk_predict", "rvk_predict_device",
            "rvk_solve_kepler", "rvk_set_option", "rvk_stream", "rvk_sync", "rvk_device_count",
-           "rvk_last_error", "rvk_version"]
+           "rvk_last_error", "rvk_version",
+           "rvk_post_create", "rvk_post_destroy", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
+           "rvk_stretch_run"]
 
 OPT_SOLVER = 1
 
 PRED_TREND = 0x0100
 PRED_GAMMA = 0x0200
+
+# include/rvk_post.h
+PRIOR_NPAR = 8
+PRIOR_KIND = {"Uniform": 0, "EccentricityUniform": 1, "Normal": 2, "TruncatedNormal": 3, "HalfNormal": 4,
+              "Rayleigh": 5, "VanEylen19Mixture": 6, "Beta": 7}
+
+
+POST_CONVERT = 1
+
+
+def prior_src_default(planet: int, j: int) -> int:
+    """RVK_PRIOR_SRC_DEFAULT: default parameter j (P K e w Tp) of planet `planet`, converted."""
+    return -(1 + 5 * planet + j)
 
 _lib = None
 
@@ -64,8 +79,18 @@ def load() -> C.CDLL:
     L.rvk_device_count.argtypes = []
     L.rvk_last_error.restype = C.c_char_p
     L.rvk_version.restype = C.c_int
+    L.rvk_post_create.argtypes = [vp, C.c_int32, ip, dp, C.c_int32, ip, ip, dp, C.c_double, C.c_double, C.c_int32]
+    L.rvk_post_create.restype = vp
+    L.rvk_post_destroy.argtypes = [vp]
+    L.rvk_post_destroy.restype = None
+    L.rvk_post_reserve.argtypes = [vp, C.c_int64]
+    L.rvk_logpost.argtypes = [vp, dp, C.c_int64, C.c_int64, dp]
+    L.rvk_logpost_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
+    L.rvk_stretch_run.argtypes = [vp, vp, vp, C.c_int64, C.c_int32, C.c_double, C.c_uint64, C.c_uint64,
+                                  vp, vp, vp, vp, vp, vp, vp, vp, vp]
     for name in ("rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
-                 "rvk_set_option", "rvk_reserve"):
+                 "rvk_set_option", "rvk_reserve", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
+                 "rvk_stretch_run"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -24,14 +24,12 @@
 #include <type_traits>
 #include <vector>
 
-#include "../../include/rvk.h"
-#include "rvk_math.h"
+#include "rvk_internal.h"
 
 using namespace rvk;
 
 namespace {
 
-constexpr int kBlock = 256;          // 4 waves
 #ifndef RVK_CHI_NR2
 #define RVK_CHI_NR2 0
 #endif
@@ -41,18 +39,6 @@ constexpr int kBlock = 256;          // 4 waves
 #ifndef RVK_LB_WAVES
 #define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
-constexpr int kWavesPerBlock = kBlock / 64;
-
-// Per-epoch data: SoA, device-resident for the handle's lifetime.
-struct EpochData {
-    const double *t;      // time
-    const double *vel;
-    const double *s2;     // velerr^2 (fit.py:3598)
-    const int32_t *inst;  // instrument index (fit.py:3586)
-    const SC *tab;        // sin/cos table (rvk_math.h, kTabN entries)
-    double t0;            // Trend reference time (model.py:486,491)
-    int par;              // parameterisation code (RVK_PAR_*)
-};
 
 // Copy the sin/cos table into LDS (whole block; one barrier, before any
 // per-wave work so no wave can skip it).
@@ -81,7 +67,8 @@ struct PassCfg {
 template <int NP, bool MULTI, int SOLVER, bool TP>
 __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
-                                                         long long stride, int wb, double *__restrict__ out) {
+                                                         long long stride, int wb, double *__restrict__ out,
+                                                         PostArgs post) {
     constexpr int WB = PassCfg<NP>::WB;
     __shared__ PlanetK pks[WB][NP];
     __shared__ int okp[WB][NP];
@@ -121,7 +108,8 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             bool all_ok = true;
 #pragma unroll
             for (int p = 0; p < NP; ++p) all_ok &= okp[j][p] != 0;
-            if (!all_ok) {
+            const double lpw = post.lp ? post.lp[w] : 0.0;   // log-prior (posterior mode)
+            if (!all_ok || lpw == -INFINITY) {
                 if (lane == 0) out[w] = -INFINITY;
                 continue;
             }
@@ -184,7 +172,9 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                 if (special) lsum = log(prod) + (double)expo * kLn2;
             }
             double tot = wave_sum(chi2 + lsum);
-            if (lane == 0) out[w] = -0.5 * (tot + (double)n_epochs * kLog2Pi);
+            double res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
+            if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
+            if (lane == 0) out[w] = res;
         }
         if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // pks/okp are rewritten next pass
     }
@@ -250,27 +240,13 @@ __global__ __launch_bounds__(256) void kepler_kernel(const double *__restrict__ 
 
 thread_local std::string g_err;
 
-int fail(int code, const std::string &msg) {
-    g_err = msg;
-    return code;
-}
-
-#define HIPCHK(expr)                                                                      \
-    do {                                                                                  \
-        hipError_t _e = (expr);                                                           \
-        if (_e != hipSuccess)                                                             \
-            return fail(RVK_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
-    } while (0)
-
-typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long, double *);
-
 // Grid: one pass per block when W is small (4 walkers per block = 1 per wave);
 // for large W at most kMaxBlocks blocks, each looping over passes of <= WB walkers.
 constexpr long long kMaxBlocks = 2048;
 
 template <int NP, bool MULTI, int SOLVER, bool TP>
 void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
-               double *out) {
+               double *out, PostArgs post) {
     constexpr int WB = PassCfg<NP>::WB;
     long long blocks = (W + kWavesPerBlock - 1) / kWavesPerBlock;
     int wb = kWavesPerBlock;
@@ -282,7 +258,7 @@ void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, lon
         if (blocks > kMaxBlocks) blocks = kMaxBlocks;
     }
     hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n, ni,
-                       th, W, stride, wb, out);
+                       th, W, stride, wb, out, post);
 }
 
 template <bool MULTI, int SOLVER, bool TP>
@@ -343,20 +319,11 @@ dim3 wave_grid(long long items) {
 
 }  // namespace
 
-struct rvk_handle {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    int n = 0, n_inst = 1, n_planets = 1, par = 0;
-    double t0 = 0.0;
-    double *d_t = nullptr, *d_vel = nullptr, *d_s2 = nullptr;
-    SC *d_tab = nullptr;
-    int32_t *d_inst = nullptr;
-    // scratch for the host-buffer entry points
-    double *d_theta = nullptr, *d_out = nullptr;
-    size_t cap_theta = 0, cap_out = 0;
-    loglike_launch_t launch = nullptr;
-    int solver = 0;
-};
+int rvk::fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
 
 extern "C" {
 
@@ -502,8 +469,7 @@ int rvk_loglike_device(rvk_handle *h, const double *d_theta, int64_t W, int64_t 
     if (!d_theta || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     hipStream_t st = (hipStream_t)stream;   // used as given: NULL is HIP's default stream
     HIPCHK(hipSetDevice(h->device));
-    EpochData d{h->d_t, h->d_vel, h->d_s2, h->d_inst, h->d_tab, h->t0, h->par};
-    h->launch(st, d, h->n, h->n_inst, d_theta, W, stride, d_out);
+    h->launch(st, h->epochs(), h->n, h->n_inst, d_theta, W, stride, d_out, PostArgs{nullptr, 0.0, 0.0});
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

@@ -1,0 +1,71 @@
+// rvk_internal.h -- declarations shared by the translation units of librvk.so
+// (rvk.hip: log-likelihood / predictive / Kepler; rvk_post.hip: device
+// log-posterior and stretch-move sampler).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/rvk.h"
+#include "rvk_math.h"
+
+namespace rvk {
+
+constexpr int kBlock = 256;                    // 4 waves
+constexpr int kWavesPerBlock = kBlock / 64;
+
+// Per-epoch data: SoA, device-resident for the handle's lifetime.
+struct EpochData {
+    const double *t;      // time
+    const double *vel;
+    const double *s2;     // velerr^2 (fit.py:3598)
+    const int32_t *inst;  // instrument index (fit.py:3586)
+    const SC *tab;        // sin/cos table (rvk_math.h, kTabN entries)
+    double t0;            // Trend reference time (model.py:486,491)
+    int par;              // parameterisation code (RVK_PAR_*)
+};
+
+// Optional log-posterior epilogue of the log-likelihood kernel (fit.py:3461-3495):
+// lp == nullptr: out = log-likelihood.  Otherwise lp[w] is the walker's log-prior
+// (-inf = rejected before the likelihood: negative jitter, a prior-side conversion
+// error or a non-finite prior), and out = ((ll + lp) + jac) + renorm in the
+// reference's order; a rejected walker skips its epoch loop.
+struct PostArgs {
+    const double *lp;
+    double jac;
+    double renorm;
+};
+
+typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long, double *,
+                                 PostArgs);
+
+int fail(int code, const std::string &msg);
+
+}  // namespace rvk
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return rvk::fail(RVK_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+    } while (0)
+
+struct rvk_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n = 0, n_inst = 1, n_planets = 1, par = 0;
+    double t0 = 0.0;
+    double *d_t = nullptr, *d_vel = nullptr, *d_s2 = nullptr;
+    rvk::SC *d_tab = nullptr;
+    int32_t *d_inst = nullptr;
+    // scratch for the host-buffer entry points
+    double *d_theta = nullptr, *d_out = nullptr;
+    size_t cap_theta = 0, cap_out = 0;
+    rvk::loglike_launch_t launch = nullptr;
+    int solver = 0;
+
+    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par}; }
+    int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }
+};

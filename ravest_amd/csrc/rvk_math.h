@@ -347,10 +347,15 @@ __device__ __forceinline__ bool valid_default(double P, double K, double e, doub
 // Conversion to the default parameterisation (param.py:299-362, 198-234).
 // PAR >= 0: compile-time parameterisation (PAR = 0 needs no atan/tan/atan2);
 // PAR = -1: runtime `par`.
+// One planet's parameters in parameterisation `par` -> the default "P K e w Tp"
+// (param.py:159-297, convert_pars_to_default_parameterisation).  Returns false
+// exactly where that conversion raises (Tc -> Tp validates e, param.py:208-209).
 template <int PAR>
-__device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, int par = PAR) {
+__device__ __forceinline__ bool to_default_t(const double *p5, double &P, double &K, double &e, double &w,
+                                             double &Tp, int par = PAR) {
     if (PAR >= 0) par = PAR;
-    double P = p5[0], K = p5[1], e, w, Tp;
+    P = p5[0];
+    K = p5[1];
     if (par >= 2) {                       // secosw/sesinw -> e, w  (param.py:217-234)
         double u = p5[2], v = p5[3];
         e = u * u + v * v;
@@ -375,6 +380,13 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
     } else {
         Tp = p5[4];
     }
+    return ok;
+}
+
+template <int PAR>
+__device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, int par = PAR) {
+    double P, K, e, w, Tp;
+    bool ok = to_default_t<PAR>(p5, P, K, e, w, Tp, par);
     ok = ok && valid_default(P, K, e, w);
     if (!ok) {                            // keep the masked walker's arithmetic finite
         P = 1.0; e = 0.0; w = 0.0;

@@ -17,13 +17,15 @@ conversion ValueError, a non-finite log-prior, or an invalid planet give -inf.
 """
 from __future__ import annotations
 
+import ctypes as C
 import logging
 from typing import Callable, Dict
 
 import numpy as np
 
+from . import _lib
 from .param import Parameterisation, full_param_names
-from .prior import Uniform, logpdf_vec
+from .prior import Uniform, device_params, logpdf_vec
 
 
 class LogLikelihood:
@@ -252,6 +254,10 @@ class LogPosterior:
                     params_for_prior[key] = value
         return params_for_prior
 
+    def device_posterior(self) -> "DevicePosterior":
+        """The same log-posterior evaluated wholly on the GPU (priors included)."""
+        return DevicePosterior(self)
+
     def _negative_log_probability_for_MAP(self, free_params_vals) -> float:
         """fit.py:3497-3526."""
         logprob = self.log_probability(dict(zip(self.free_params_names, free_params_vals)))
@@ -259,3 +265,84 @@ class LogPosterior:
         if not np.isfinite(neg):
             return 1e30
         return neg
+
+
+class DevicePosterior:
+    """``LogPosterior`` evaluated wholly on the GPU (include/rvk_post.h).
+
+    The host builds, once, what ``LogPosterior.log_probability`` recomputes per
+    call: the fixed/free layout, the prior slots in the reference's key order
+    (fit.py:3426-3444 dict order) with each prior's constants, and the two
+    correction constants.  ``__call__`` (host arrays) and ``device`` (torch
+    tensors, stream-ordered) then run the jitter check, the prior-side conversion,
+    the priors, the log-likelihood and the corrections in two kernels.  Only the
+    built-in priors have a device form; a custom callable prior raises
+    NotImplementedError (use ``LogPosterior.log_probability_batch``)."""
+
+    def __init__(self, lpost: "LogPosterior") -> None:
+        self.lpost = lpost
+        eng = lpost.log_likelihood.engine
+        self.engine = eng
+        names = lpost._names
+        self.n_free = len(lpost.free_params_names)
+        kinds, srcs, pars = [], [], []
+        conv_keys = {f"{dp}_{L}": (i, j) for i, L in enumerate(lpost.planet_letters)
+                     for j, dp in enumerate(("P", "K", "e", "w", "Tp"))}
+        for k in lpost._prior_order:
+            kind, p = device_params(lpost.priors[k])
+            kinds.append(kind)
+            pars.append(p)
+            if lpost._case3 and k in conv_keys:
+                srcs.append(_lib.prior_src_default(*conv_keys[k]))
+            else:
+                srcs.append(names.index(k))
+        self._kinds = np.ascontiguousarray(kinds, np.int32)
+        self._srcs = np.ascontiguousarray(srcs, np.int32)
+        self._pars = np.ascontiguousarray(np.reshape(pars, (-1, _lib.PRIOR_NPAR)), np.float64)
+        self._free_idx = np.ascontiguousarray(lpost._free_idx, np.int32)
+        tmpl = np.nan_to_num(lpost._template, nan=0.0)            # free columns are overwritten per walker
+        self._tmpl = np.ascontiguousarray(tmpl, np.float64)
+        flags = _lib.POST_CONVERT if lpost._case3 else 0
+        L = _lib.load()
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        self._p = L.rvk_post_create(eng._h, self.n_free, self._free_idx.ctypes.data_as(ip),
+                                    self._tmpl.ctypes.data_as(dp), len(kinds), self._kinds.ctypes.data_as(ip),
+                                    self._srcs.ctypes.data_as(ip), self._pars.ctypes.data_as(dp),
+                                    float(lpost._logprob_jacobian_correction),
+                                    float(lpost._logprob_prior_renorm_correction), flags)
+        if not self._p:
+            raise _lib.RVKError(f"rvk_post_create failed: {_lib.last_error()}")
+
+    def __call__(self, theta_free) -> np.ndarray:
+        theta_free = np.ascontiguousarray(np.atleast_2d(np.asarray(theta_free, dtype=np.float64)))
+        if theta_free.shape[1] != self.n_free:
+            raise ValueError(f"expected {self.n_free} free parameters, got {theta_free.shape[1]}")
+        out = np.empty(theta_free.shape[0])
+        dp = C.POINTER(C.c_double)
+        _lib.check(_lib.load().rvk_logpost(self._p, theta_free.ctypes.data_as(dp), theta_free.shape[0],
+                                           theta_free.shape[1], out.ctypes.data_as(dp)))
+        return out
+
+    def device(self, theta_free, out, stream=None) -> None:
+        """theta_free: float64 cuda tensor [W, >= n_free] (unit column stride); out: float64 [W]."""
+        import torch
+        assert theta_free.dtype == torch.float64 and out.dtype == torch.float64
+        assert theta_free.is_cuda and theta_free.stride(1) == 1 and out.is_contiguous()
+        if stream is None:
+            stream = torch.cuda.current_stream(theta_free.device)
+        _lib.check(_lib.load().rvk_logpost_device(self._p, theta_free.data_ptr(), theta_free.shape[0],
+                                                  theta_free.stride(0), out.data_ptr(), stream.cuda_stream))
+
+    def reserve(self, max_walkers: int) -> None:
+        _lib.check(_lib.load().rvk_post_reserve(self._p, int(max_walkers)))
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            _lib.load().rvk_post_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

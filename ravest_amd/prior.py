@@ -245,3 +245,45 @@ def logpdf_vec(prior, x) -> np.ndarray:
         return prior.logpdf(x)
     x = _arr(x)
     return np.array([float(prior(float(v))) for v in x.ravel()]).reshape(x.shape)
+
+
+# ---- device form (include/rvk_post.h RVK_PRIOR_*) --------------------------------------------
+try:
+    from scipy.stats._continuous_distns import _norm_pdf_logC as _LOG_SQRT_2PI
+except ImportError:  # pragma: no cover - same expression as scipy's
+    _LOG_SQRT_2PI = float(np.log(np.sqrt(2 * np.pi)))
+_HALF_LOG_2_OVER_PI = float(0.5 * np.log(2.0 / np.pi))    # scipy halfnorm._logpdf constant
+
+
+def device_params(prior):
+    """(kind, p[8]) of a built-in prior for the device log-posterior: the constants the
+    reference computes once (or scipy computes per call), evaluated here with the same
+    expressions, so the device repeats the reference's arithmetic.  A prior that is not
+    one of the built-in classes raises NotImplementedError: custom callables stay on the
+    host path (posterior.LogPosterior.log_probability_batch)."""
+    from . import _lib
+    p = np.zeros(_lib.PRIOR_NPAR)
+    name = type(prior).__name__
+    if isinstance(prior, Uniform):
+        p[:3] = prior.lower, prior.upper, -np.log(prior.upper - prior.lower)
+    elif isinstance(prior, EccentricityUniform):
+        p[:2] = prior.upper, -np.log(prior.upper)
+    elif isinstance(prior, Normal):
+        p[:3] = prior.mean, prior.std, prior._log_norm_const
+    elif isinstance(prior, TruncatedNormal):
+        from scipy.stats._continuous_distns import _log_gauss_mass
+        p[:7] = (prior.mean, prior.std, prior.lower, prior.upper, _LOG_SQRT_2PI,
+                 float(_log_gauss_mass(np.float64(prior._a), np.float64(prior._b))), np.log(prior.std))
+    elif isinstance(prior, HalfNormal):
+        p[:3] = prior.std, np.log(prior.std), _HALF_LOG_2_OVER_PI
+    elif isinstance(prior, Rayleigh):
+        p[:2] = prior.scale, np.log(prior.scale)
+    elif isinstance(prior, VanEylen19Mixture):
+        p[:7] = (prior.sigma_normal, np.log(prior.sigma_normal), prior.sigma_rayleigh, np.log(prior.sigma_rayleigh),
+                 1 - prior.f, prior.f, _HALF_LOG_2_OVER_PI)
+    elif isinstance(prior, Beta):
+        p[:3] = prior.a, prior.b, prior._log_beta
+    else:
+        raise NotImplementedError(f"prior {prior!r} ({name}) has no device form; built-in priors: "
+                                  f"{PRIOR_FUNCTIONS}")
+    return _lib.PRIOR_KIND[name], p

@@ -10,9 +10,13 @@ from tests.conftest import ROOT
 
 
 def _declared():
-    src = open(os.path.join(ROOT, "include", "rvk.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(rvk_[a-z_]+)\s*\(", src)))
+    names = set()
+    for hdr in ("rvk.h", "rvk_post.h"):
+        src = open(os.path.join(ROOT, "include", hdr)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"#define.*", "", src)
+        names |= set(re.findall(r"\b(rvk_[a-z_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_header_and_library_agree():
@@ -50,6 +54,12 @@ def test_bad_arguments_fail_loudly():
     h = L.rvk_create(t.ctypes.data_as(dp), t.ctypes.data_as(dp), t.ctypes.data_as(dp), None, 8, 2, 1, 0, 0.0, -1)
     assert not h and "inst_idx" in _lib.last_error()
     assert L.rvk_loglike(None, None, 1, 9, None) == -1
+    # the posterior / sampler entry points check their arguments before touching a device
+    assert not L.rvk_post_create(None, 1, None, None, 0, None, None, None, 0.0, 0.0, 0)
+    assert "handle" in _lib.last_error()
+    assert L.rvk_logpost_device(None, None, 1, 1, None, None) == -1
+    assert L.rvk_stretch_run(None, None, None, 8, 1, 2.0, 0, 0, None, None, None, None, None, None, None, None,
+                             None) == -1
 
 
 def test_engine_raises_without_library(monkeypatch, tmp_path):

@@ -2,7 +2,7 @@
 import numpy as np
 import pytest
 
-from ravest_amd.sampler import EnsembleSampler
+from ravest_amd.sampler import EnsembleSampler, emcee_step_draws
 
 
 def test_gaussian_moments():
@@ -34,3 +34,20 @@ def test_minus_inf_rejects_nan_raises():
     s2 = EnsembleSampler(8, 2, lambda x: np.full(len(x), np.nan), seed=3)
     with pytest.raises(ValueError):
         s2.run_mcmc(np.zeros((8, 2)), 1)
+
+
+def test_emcee_call_order():
+    """The draws are emcee 3.1's, in its order: shuffle(inds % 2), then per half rand(H),
+    randint(H, size=H), H x rand()."""
+    W, H = 10, 5
+    a = np.random.RandomState(42)
+    sets, zu, rint, au = emcee_step_draws(a, W)
+    b = np.random.RandomState(42)
+    inds = np.arange(W) % 2
+    b.shuffle(inds)
+    for split in (0, 1):
+        assert np.array_equal(sets[split], np.arange(W)[inds == split])
+        assert np.array_equal(zu[split], b.rand(H))
+        assert np.array_equal(rint[split], b.randint(H, size=(H,)))
+        assert np.array_equal(au[split], np.array([b.rand() for _ in range(H)]))
+    assert np.array_equal(np.sort(np.concatenate(sets)), np.arange(W))
