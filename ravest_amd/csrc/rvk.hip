@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "rvk_internal.h"
+#include "rvk_post_dev.h"
 
 using namespace rvk;
 
@@ -59,16 +60,20 @@ __device__ __forceinline__ void load_tab(SC *lds, const SC *__restrict__ g) {
 //   3. wave wv evaluates walkers wv, wv+4, ... of the pass: lanes stride the
 //      epochs, planet constants are re-read from LDS with a wave-uniform
 //      address (broadcast), a wave64 butterfly gives the walker's sum.
+//
+// SAMPLE (rvk_stretch_run): the rows are the proposals of the active half
+// (propose_kernel), lp their log-priors; after the reduction the wave accepts
+// or rejects its proposal and writes the walker's state and chain row.
 template <int NP>
 struct PassCfg {
     static constexpr int WB = (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
 };
 
-template <int NP, bool MULTI, int SOLVER, bool TP>
+template <int NP, bool MULTI, int SOLVER, bool TP, bool SAMPLE>
 __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
                                                          long long stride, int wb, double *__restrict__ out,
-                                                         PostArgs post) {
+                                                         PostArgs post, SampleArgs sa) {
     constexpr int WB = PassCfg<NP>::WB;
     __shared__ PlanetK pks[WB][NP];
     __shared__ int okp[WB][NP];
@@ -94,10 +99,10 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
         for (int k = threadIdx.x; k < nb * NP; k += kBlock) {
             const int j = k / NP, p = k - j * NP;
             const long long w = base + j;
+            const double *p5 = theta + w * stride + 5 * p;
             PlanetK pk;
             // "P K e w Tp" inline (no call, no scratch); the others out of line
-            const bool ok = TP ? planet_consts_t<0>(theta + w * stride + 5 * p, pk)
-                               : planet_consts(d.par, theta + w * stride + 5 * p, pk);
+            const bool ok = TP ? planet_consts_t<0>(p5, pk) : planet_consts(d.par, p5, pk);
             pks[j][p] = pk;
             okp[j][p] = ok;
         }
@@ -105,14 +110,12 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
         for (int j = wv; j < nb; j += kWavesPerBlock) {
             const long long w = base + j;
             const double *row = theta + w * stride;
+            const double lpw = post.lp ? post.lp[w] : 0.0;      // log-prior (posterior / sampler mode)
             bool all_ok = true;
 #pragma unroll
             for (int p = 0; p < NP; ++p) all_ok &= okp[j][p] != 0;
-            const double lpw = post.lp ? post.lp[w] : 0.0;   // log-prior (posterior mode)
-            if (!all_ok || lpw == -INFINITY) {
-                if (lane == 0) out[w] = -INFINITY;
-                continue;
-            }
+            double res = -INFINITY;
+            if (all_ok && lpw != -INFINITY) {
             const double *g = row + 5 * NP;
             const double *jit = g + n_inst;
             const double gd = jit[n_inst], gdd = jit[n_inst + 1];
@@ -172,11 +175,34 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                 if (special) lsum = log(prod) + (double)expo * kLn2;
             }
             double tot = wave_sum(chi2 + lsum);
-            double res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
+            res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
             if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
-            if (lane == 0) out[w] = res;
+            }
+            if constexpr (SAMPLE) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
+                const int D = sa.D;
+                const long long sw = sa.sidx[w];
+                const double lp_old = sa.lp[sw];
+                const bool acc = sa.fac[w] + res - lp_old > log(sa.au[w]);
+                double *xs = sa.x + sw * D;
+                const double *qw = sa.q + w * D;
+                if (lane == 0 && isnan(res)) atomicOr(sa.status, 1);
+                for (int c = lane; c < D; c += 64) {
+                    const double v = acc ? qw[c] : xs[c];
+                    if (acc) xs[c] = v;
+                    if (sa.chain) sa.chain[sw * D + c] = v;
+                }
+                if (lane == 0) {
+                    if (acc) {
+                        sa.lp[sw] = res;
+                        if (sa.nacc) sa.nacc[sw] += 1;
+                    }
+                    if (sa.lnpc) sa.lnpc[sw] = acc ? res : lp_old;
+                }
+            } else {
+                if (lane == 0) out[w] = res;
+            }
         }
-        if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // pks/okp are rewritten next pass
+        if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // LDS rows are rewritten next pass
     }
 }
 
@@ -244,12 +270,11 @@ thread_local std::string g_err;
 // for large W at most kMaxBlocks blocks, each looping over passes of <= WB walkers.
 constexpr long long kMaxBlocks = 2048;
 
-template <int NP, bool MULTI, int SOLVER, bool TP>
-void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
-               double *out, PostArgs post) {
+template <int NP>
+void ll_grid(long long W, long long &blocks, int &wb) {
     constexpr int WB = PassCfg<NP>::WB;
-    long long blocks = (W + kWavesPerBlock - 1) / kWavesPerBlock;
-    int wb = kWavesPerBlock;
+    blocks = (W + kWavesPerBlock - 1) / kWavesPerBlock;
+    wb = kWavesPerBlock;
     if (blocks > kMaxBlocks) {
         long long per = (W + kMaxBlocks - 1) / kMaxBlocks;                 // walkers per block
         per = ((per + kWavesPerBlock - 1) / kWavesPerBlock) * kWavesPerBlock;
@@ -257,8 +282,27 @@ void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, lon
         blocks = (W + wb - 1) / wb;
         if (blocks > kMaxBlocks) blocks = kMaxBlocks;
     }
-    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n, ni,
-                       th, W, stride, wb, out, post);
+}
+
+template <int NP, bool MULTI, int SOLVER, bool TP>
+void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
+               double *out, PostArgs post) {
+    long long blocks;
+    int wb;
+    ll_grid<NP>(W, blocks, wb);
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d,
+                       n, ni, th, W, stride, wb, out, post, SampleArgs{});
+}
+
+// The fused stretch-move half-step over the H walkers of the active half (SOLVER 0 only).
+template <int NP, bool MULTI, bool TP>
+void launch_sample(hipStream_t st, EpochData d, int n, int ni, const double *rows, long long H, long long stride,
+                   PostArgs post, const SampleArgs &sa) {
+    long long blocks;
+    int wb;
+    ll_grid<NP>(H, blocks, wb);
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
+                       ni, rows, H, stride, wb, nullptr, post, sa);
 }
 
 template <bool MULTI, int SOLVER, bool TP>
@@ -284,6 +328,26 @@ loglike_launch_t pick_ll_t(int np, bool multi) {
 loglike_launch_t pick_ll(int np, bool multi, int solver, bool tp) {
     if (solver == 1) return tp ? pick_ll_t<1, true>(np, multi) : pick_ll_t<1, false>(np, multi);
     return tp ? pick_ll_t<0, true>(np, multi) : pick_ll_t<0, false>(np, multi);
+}
+
+template <bool MULTI, bool TP>
+sample_launch_t pick_sample_s(int np) {
+    switch (np) {
+        case 1: return launch_sample<1, MULTI, TP>;
+        case 2: return launch_sample<2, MULTI, TP>;
+        case 3: return launch_sample<3, MULTI, TP>;
+        case 4: return launch_sample<4, MULTI, TP>;
+        case 5: return launch_sample<5, MULTI, TP>;
+        case 6: return launch_sample<6, MULTI, TP>;
+        case 7: return launch_sample<7, MULTI, TP>;
+        case 8: return launch_sample<8, MULTI, TP>;
+        default: return nullptr;
+    }
+}
+
+sample_launch_t pick_sample(int np, bool multi, bool tp) {
+    if (multi) return tp ? pick_sample_s<true, true>(np) : pick_sample_s<true, false>(np);
+    return tp ? pick_sample_s<false, true>(np) : pick_sample_s<false, false>(np);
 }
 
 int check_gfx950(int dev) {
@@ -389,6 +453,7 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->par = par;
     h->t0 = t0;
     h->launch = pick_ll(n_planets, n_inst > 1, 0, par == RVK_PAR_PKEWTP);
+    h->sample = pick_sample(n_planets, n_inst > 1, par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;

@@ -10,6 +10,7 @@
 
 #include "../../include/rvk.h"
 #include "rvk_math.h"
+#include "rvk_post_dev.h"
 
 namespace rvk {
 
@@ -41,6 +42,9 @@ struct PostArgs {
 typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long, double *,
                                  PostArgs);
 
+typedef void (*sample_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long, PostArgs,
+                                const SampleArgs &);
+
 int fail(int code, const std::string &msg);
 
 }  // namespace rvk
@@ -64,6 +68,7 @@ struct rvk_handle {
     double *d_theta = nullptr, *d_out = nullptr;
     size_t cap_theta = 0, cap_out = 0;
     rvk::loglike_launch_t launch = nullptr;
+    rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
     int solver = 0;
 
     rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par}; }

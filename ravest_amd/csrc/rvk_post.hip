@@ -15,223 +15,96 @@
 
 #include "../../include/rvk_post.h"
 #include "rvk_internal.h"
+#include "rvk_post_dev.h"
 
 using namespace rvk;
 
 namespace {
 
-struct PriorSlot {
-    int32_t kind, src;
-    double p[RVK_PRIOR_NPAR];
-};
-
-struct PostDev {
-    int n_free, p_full, n_prior, n_planets, n_inst, par;
-    bool convert;                // convert every planet to P K e w Tp first (RVK_POST_CONVERT or a src < 0)
-    const int32_t *colmap;       // [p_full]: free position of a column, or -1 (fixed)
-    const double *tmpl;          // [p_full]
-    const PriorSlot *slots;      // [n_prior]
-};
-
-// scipy.stats halfnorm / rayleigh logpdf as scipy evaluates them (x >= 0):
-// _logpdf(x / scale) - log(scale)
-__device__ __forceinline__ double halfnorm_lp(double x, double scale, double log_scale, double c) {
-    const double y = x / scale;
-    return (c - y * y / 2.0) - log_scale;                  // 0.5*log(2/pi) - x*x/2.0
-}
-__device__ __forceinline__ double rayleigh_lp(double x, double scale, double log_scale) {
-    const double y = x / scale;
-    return (log(y) - 0.5 * y * y) - log_scale;             // log(r) - 0.5 * r * r
-}
-
-// One prior term, the reference's formula and bounds (prior.py).
-__device__ double prior_lp(const PriorSlot &s, double x) {
-    const double *p = s.p;
-    switch (s.kind) {
-        case RVK_PRIOR_UNIFORM:
-            return (x < p[0] || x > p[1]) ? -INFINITY : p[2];
-        case RVK_PRIOR_ECC_UNIFORM:
-            return (x < 0.0 || x >= p[0]) ? -INFINITY : p[1];
-        case RVK_PRIOR_NORMAL: {
-            const double y = (x - p[0]) / p[1];
-            return -0.5 * (y * y) - p[2];
-        }
-        case RVK_PRIOR_TRUNCNORM: {                      // scipy truncnorm.logpdf inside the bounds
-            if (x < p[2] || x > p[3]) return -INFINITY;
-            const double y = (x - p[0]) / p[1];
-            return ((-(y * y) / 2.0 - p[4]) - p[5]) - p[6];
-        }
-        case RVK_PRIOR_HALFNORMAL:
-            if (x < 0.0) return -INFINITY;
-            return halfnorm_lp(x, p[0], p[1], p[2]);
-        case RVK_PRIOR_RAYLEIGH:
-            if (x < 0.0) return -INFINITY;
-            return rayleigh_lp(x, p[0], p[1]);
-        case RVK_PRIOR_VANEYLEN19: {                     // scipy 1.15 logsumexp([hn, ry], b=[1-f, f])
-            if (x < 0.0) return -INFINITY;
-            const double b0 = p[4], b1 = p[5];
-            double a0 = halfnorm_lp(x, p[0], p[1], p[6]), a1 = rayleigh_lp(x, p[2], p[3]);
-            if (b0 == 0.0) a0 = -INFINITY;
-            if (b1 == 0.0) a1 = -INFINITY;
-            const double amax = (isnan(a0) || isnan(a1)) ? NAN : fmax(a0, a1);
-            const bool m0 = a0 == amax, m1 = a1 == amax;
-            const double m = b0 * (m0 ? 1.0 : 0.0) + b1 * (m1 ? 1.0 : 0.0);
-            const double shift = isfinite(amax) ? amax : 0.0;
-            double sum = b0 * exp((m0 ? -INFINITY : a0) - shift) + b1 * exp((m1 ? -INFINITY : a1) - shift);
-            sum = (sum == 0.0) ? sum : sum / m;
-            return (log1p(sum) + log(m)) + amax;
-        }
-        case RVK_PRIOR_BETA: {                           // xlogy(a-1, x) + xlog1py(b-1, -x) - log B
-            if (x < 0.0 || x > 1.0) return -INFINITY;
-            const double am1 = p[0] - 1.0, bm1 = p[1] - 1.0;
-            const double t1 = (am1 == 0.0 && !isnan(x)) ? 0.0 : am1 * log(x);
-            const double t2 = (bm1 == 0.0 && !isnan(x)) ? 0.0 : bm1 * log1p(-x);
-            return (t1 + t2) - p[2];
-        }
-        default:
-            return NAN;
-    }
-}
-
-// ---- Philox4x32-10 (counter-based; Salmon et al. 2011) -------------------------------
-__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-        k.x += 0x9E3779B9u;
-        k.y += 0xBB67AE85u;
-    }
-    return c;
-}
-// 53-bit uniform in [0, 1) from two words (numpy's construction)
-__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
-}
-
-// Draws of one (step, half, walker-in-half).
-struct Draw {
-    long long s, c;     // active walker, complementary walker
-    double zu, au;
-};
-
-struct RngArgs {
-    const int32_t *set;   // [steps][2][H] or nullptr (Philox)
-    const double *zu;
-    const int32_t *rint;
-    const double *au;
-    uint64_t seed, step0;
-};
-
-__device__ __forceinline__ Draw draw(const RngArgs &r, int step, int half, long long j, long long H) {
-    Draw d;
-    if (r.set) {
-        const long long o = ((long long)step * 2 + half) * H + j;
-        const long long ob = ((long long)step * 2 + (1 - half)) * H;
-        d.s = r.set[o];
-        d.c = r.set[ob + r.rint[o]];
-        d.zu = r.zu[o];
-        d.au = r.au[o];
-    } else {
-        const uint64_t st = r.step0 + (uint64_t)step;
-        const uint2 key = make_uint2((uint32_t)r.seed, (uint32_t)(r.seed >> 32));
-        const uint4 a = philox(make_uint4((uint32_t)j, (uint32_t)half, (uint32_t)st, (uint32_t)(st >> 32)), key);
-        const uint4 b = philox(make_uint4((uint32_t)j, (uint32_t)half | 2u, (uint32_t)st, (uint32_t)(st >> 32)), key);
-        d.s = (long long)half * H + j;
-        // complement index in [0, H): multiply-shift (bias <= H / 2^32)
-        d.c = (long long)(1 - half) * H + (long long)(((uint64_t)b.x * (uint64_t)H) >> 32);
-        d.zu = u53(a.x, a.y);
-        d.au = u53(a.z, a.w);
-    }
-    return d;
-}
-
-// Per-walker prologue: x (n_free coordinates) -> full row + log-prior.
-__device__ void post_row(const PostDev &pd, const double *x, double *full, double *lp_out) {
-    for (int c = 0; c < pd.p_full; ++c) {
-        const int f = pd.colmap[c];
-        full[c] = f >= 0 ? x[f] : pd.tmpl[c];
-    }
-    bool dead = false;
-    const int jit0 = 5 * pd.n_planets + pd.n_inst;
-    for (int k = 0; k < pd.n_inst; ++k) dead |= full[jit0 + k] < 0.0;   // fit.py:3465-3468
-    double def[RVK_MAX_PLANETS][5];
-    if (pd.convert) {                                                   // fit.py:3426-3444
-        for (int p = 0; p < pd.n_planets; ++p) {
-            const bool ok = to_default_t<-1>(full + 5 * p, def[p][0], def[p][1], def[p][2], def[p][3], def[p][4],
-                                             pd.par);
-            dead |= !ok;                                                // ValueError -> -inf
-        }
-    }
-    double lp = 0.0;                                                    // fit.py:3684-3691
-    for (int k = 0; k < pd.n_prior; ++k) {
-        const PriorSlot &s = pd.slots[k];
-        double v;
-        if (s.src >= 0) {
-            v = full[s.src];
-        } else {
-            const int q = -s.src - 1;
-            v = def[q / 5][q % 5];
-        }
-        lp += prior_lp(s, v);
-    }
-    if (!isfinite(lp)) dead = true;                                     // fit.py:3481-3482
-    *lp_out = dead ? -INFINITY : lp;
-}
-
+// Log-prior + full rows of a walker block (rvk_logpost_device): one wave per walker.
 __global__ __launch_bounds__(256) void logprior_kernel(PostDev pd, const double *__restrict__ xf, long long W,
                                                        long long stride, double *__restrict__ full,
                                                        double *__restrict__ lp) {
-    const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
-    post_row(pd, xf + w * stride, full + w * pd.p_full, lp + w);
+    __shared__ PostWaveLds lds[kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    PostWaveLds &L = lds[wv];
+    for (long long w = (long long)blockIdx.x * kWavesPerBlock + wv; w < W; w += (long long)gridDim.x * kWavesPerBlock) {
+        for (int c = lane; c < pd.n_free; c += 64) L.x[c] = xf[w * stride + c];
+        wave_lds_sync();
+        const double v = post_row_wave(pd, L, full + w * pd.p_full);
+        if (lane == 0) lp[w] = v;
+        wave_lds_sync();
+    }
 }
 
-// Stretch-move proposal for the walkers of one half (emcee StretchMove.get_proposal):
-// q = c - (c - s) * z, z = ((a - 1) u + 1)^2 / a, factor = (ndim - 1) log z.
+// Stretch-move proposals of one half (emcee StretchMove.get_proposal), one wave per
+// proposal: q = c - (c - s) * z, z = ((a - 1) u + 1)^2 / a, factor = (ndim - 1) log z;
+// then its full row and log-prior.  The accept / reject runs in the epilogue of the
+// log-likelihood kernel (SAMPLE mode) or in accept_kernel.
 __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, RngArgs rng, int step, int half, long long H,
                                                       double a, const double *__restrict__ x,
                                                       double *__restrict__ q, double *__restrict__ full,
-                                                      double *__restrict__ lp, double *__restrict__ fac) {
-    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= H) return;
-    const Draw d = draw(rng, step, half, j, H);
-    const double zt = (a - 1.0) * d.zu + 1.0;
-    const double z = zt * zt / a;
+                                                      double *__restrict__ lp, double *__restrict__ fac,
+                                                      double *__restrict__ au, long long *__restrict__ sidx) {
+    __shared__ PostWaveLds lds[kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    PostWaveLds &L = lds[wv];
     const int D = pd.n_free;
-    const double *xs = x + d.s * D, *xc = x + d.c * D;
-    double *qj = q + j * D;
-    for (int k = 0; k < D; ++k) qj[k] = xc[k] - (xc[k] - xs[k]) * z;
-    fac[j] = ((double)D - 1.0) * log(z);
-    post_row(pd, qj, full + j * pd.p_full, lp + j);
+    for (long long j = (long long)blockIdx.x * kWavesPerBlock + wv; j < H; j += (long long)gridDim.x * kWavesPerBlock) {
+        const Draw d = draw(rng, step, half, j, H);
+        const double zt = (a - 1.0) * d.zu + 1.0;
+        const double z = zt * zt / a;
+        const double *xs = x + d.s * D, *xc = x + d.c * D;
+        for (int c = lane; c < D; c += 64) {
+            const double v = xc[c] - (xc[c] - xs[c]) * z;
+            L.x[c] = v;
+            q[j * D + c] = v;
+        }
+        wave_lds_sync();
+        const double v = post_row_wave(pd, L, full + j * pd.p_full);
+        if (lane == 0) {
+            lp[j] = v;
+            fac[j] = ((double)D - 1.0) * log(z);
+            au[j] = d.au;
+            sidx[j] = d.s;
+        }
+        wave_lds_sync();
+    }
 }
 
-// Accept / reject (RedBlueMove.propose + update) and the chain write of the half.
-__global__ __launch_bounds__(256) void accept_kernel(RngArgs rng, int step, int half, long long H, int D,
-                                                     const double *__restrict__ q, const double *__restrict__ fac,
+// Accept / reject (RedBlueMove.propose + update) and the chain write of the half, for the
+// unfused path (reference solver): one thread per proposal.
+__global__ __launch_bounds__(256) void accept_kernel(long long H, int D, const double *__restrict__ q,
+                                                     const double *__restrict__ fac, const double *__restrict__ au,
+                                                     const long long *__restrict__ sidx,
                                                      const double *__restrict__ nlp_all, double *__restrict__ x,
                                                      double *__restrict__ lp, long long *__restrict__ nacc,
                                                      double *__restrict__ chain, double *__restrict__ lnpc,
                                                      int *__restrict__ status) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= H) return;
-    const Draw d = draw(rng, step, half, j, H);
+    const long long s = sidx[j];
     const double nlp = nlp_all[j];
     if (isnan(nlp)) atomicOr(status, 1);
-    const double lnpdiff = fac[j] + nlp - lp[d.s];
-    double *xs = x + d.s * D;
-    if (lnpdiff > log(d.au)) {
+    const double lnpdiff = fac[j] + nlp - lp[s];
+    double *xs = x + s * D;
+    if (lnpdiff > log(au[j])) {
         for (int k = 0; k < D; ++k) xs[k] = q[j * D + k];
-        lp[d.s] = nlp;
-        if (nacc) nacc[d.s] += 1;
+        lp[s] = nlp;
+        if (nacc) nacc[s] += 1;
     }
     if (chain)
-        for (int k = 0; k < D; ++k) chain[d.s * D + k] = xs[k];
-    if (lnpc) lnpc[d.s] = lp[d.s];
+        for (int k = 0; k < D; ++k) chain[s * D + k] = xs[k];
+    if (lnpc) lnpc[s] = lp[s];
 }
 
 unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
+
+// one wave per item, at most 2^16 blocks (grid-stride beyond)
+unsigned wave_blocks(long long n) {
+    long long b = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
+}
 
 }  // namespace
 
@@ -245,7 +118,8 @@ struct rvk_post {
     PriorSlot *d_slots = nullptr;
     // workspace, sized for cap walkers
     long long cap = 0;
-    double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr;
+    double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_au = nullptr;
+    long long *d_sidx = nullptr;
 
     PostDev dev() const {
         return PostDev{n_free, h->p_full(), n_prior, h->n_planets, h->n_inst, h->par, convert, d_colmap, d_tmpl,
@@ -264,6 +138,8 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
     (void)hipFree(p->d_nlp);
+    (void)hipFree(p->d_au);
+    (void)hipFree(p->d_sidx);
     delete p;
 }
 
@@ -275,7 +151,10 @@ static int reserve_impl(rvk_post *p, long long W) {
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
     (void)hipFree(p->d_nlp);
-    p->d_full = p->d_lp = p->d_q = p->d_fac = p->d_nlp = nullptr;
+    (void)hipFree(p->d_au);
+    (void)hipFree(p->d_sidx);
+    p->d_full = p->d_lp = p->d_q = p->d_fac = p->d_nlp = p->d_au = nullptr;
+    p->d_sidx = nullptr;
     p->cap = 0;
     const size_t w = (size_t)W;
     HIPCHK(hipMalloc(&p->d_full, sizeof(double) * w * (size_t)p->h->p_full()));
@@ -283,6 +162,8 @@ static int reserve_impl(rvk_post *p, long long W) {
     HIPCHK(hipMalloc(&p->d_q, sizeof(double) * w * (size_t)(p->n_free > 0 ? p->n_free : 1)));
     HIPCHK(hipMalloc(&p->d_fac, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_nlp, sizeof(double) * w));
+    HIPCHK(hipMalloc(&p->d_au, sizeof(double) * w));
+    HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * w));
     p->cap = W;
     return RVK_OK;
 }
@@ -365,7 +246,7 @@ int rvk_logpost_device(rvk_post *p, const double *d_free, int64_t W, int64_t str
     hipStream_t st = (hipStream_t)stream;
     rvk_handle *h = p->h;
     HIPCHK(hipSetDevice(h->device));
-    hipLaunchKernelGGL(logprior_kernel, dim3(blocks_for(W)), dim3(256), 0, st, p->dev(), d_free, (long long)W,
+    hipLaunchKernelGGL(logprior_kernel, dim3(wave_blocks(W)), dim3(256), 0, st, p->dev(), d_free, (long long)W,
                        (long long)stride, p->d_full, p->d_lp);
     h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, W, h->p_full(), d_out, PostArgs{p->d_lp, p->jac, p->renorm});
     HIPCHK(hipGetLastError());
@@ -423,12 +304,19 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
         double *ch = d_chain ? d_chain + (size_t)s * (size_t)W * (size_t)D : nullptr;
         double *lc = d_lnp ? d_lnp + (size_t)s * (size_t)W : nullptr;
         for (int half = 0; half < 2; ++half) {
-            hipLaunchKernelGGL(propose_kernel, dim3(blocks_for(H)), dim3(256), 0, st, pd, rng, s, half, H, a, d_x,
-                               p->d_q, p->d_full, p->d_lp, p->d_fac);
-            h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp,
-                      PostArgs{p->d_lp, p->jac, p->renorm});
-            hipLaunchKernelGGL(accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, rng, s, half, H, D, p->d_q,
-                               p->d_fac, p->d_nlp, d_x, d_lp, (long long *)d_naccepted, ch, lc, (int *)d_status);
+            hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, rng, s, half, H, a, d_x,
+                               p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
+            const PostArgs post{p->d_lp, p->jac, p->renorm};
+            if (h->solver == 0 && h->sample) {   // accept / reject fused into the likelihood kernel
+                const SampleArgs sa{D, p->d_q, p->d_fac, p->d_au, p->d_sidx, d_x, d_lp, (long long *)d_naccepted,
+                                    ch, lc, (int *)d_status};
+                h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
+            } else {
+                h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
+                hipLaunchKernelGGL(accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, H, D, p->d_q, p->d_fac,
+                                   p->d_au, p->d_sidx, p->d_nlp, d_x, d_lp, (long long *)d_naccepted, ch, lc,
+                                   (int *)d_status);
+            }
         }
     }
     HIPCHK(hipGetLastError());

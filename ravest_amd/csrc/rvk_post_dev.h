@@ -1,0 +1,212 @@
+// rvk_post_dev.h -- device pieces of the log-posterior and the stretch move, shared by
+// the stand-alone posterior kernels (rvk_post.hip) and the fused sampler mode of the
+// log-likelihood kernel (rvk.hip).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/rvk_post.h"
+#include "rvk_math.h"
+
+namespace rvk {
+
+constexpr int kMaxPFull = 5 * RVK_MAX_PLANETS + 2 * RVK_MAX_INST + 2;   // 74
+constexpr int kMaxPFullPad = 80;
+
+struct PriorSlot {
+    int32_t kind, src;
+    double p[RVK_PRIOR_NPAR];
+};
+
+struct PostDev {
+    int n_free, p_full, n_prior, n_planets, n_inst, par;
+    bool convert;                // convert every planet to P K e w Tp first (RVK_POST_CONVERT or a src < 0)
+    const int32_t *colmap;       // [p_full]: free position of a column, or -1 (fixed)
+    const double *tmpl;          // [p_full]
+    const PriorSlot *slots;      // [n_prior]
+};
+
+// scipy.stats halfnorm / rayleigh logpdf as scipy evaluates them (x >= 0):
+// _logpdf(x / scale) - log(scale)
+__device__ __forceinline__ double halfnorm_lp(double x, double scale, double log_scale, double c) {
+    const double y = x / scale;
+    return (c - y * y / 2.0) - log_scale;                  // 0.5*log(2/pi) - x*x/2.0
+}
+__device__ __forceinline__ double rayleigh_lp(double x, double scale, double log_scale) {
+    const double y = x / scale;
+    return (log(y) - 0.5 * y * y) - log_scale;             // log(r) - 0.5 * r * r
+}
+
+// One prior term, the reference's formula and bounds (prior.py).
+inline __device__ double prior_lp(const PriorSlot &s, double x) {
+    const double *p = s.p;
+    switch (s.kind) {
+        case RVK_PRIOR_UNIFORM:
+            return (x < p[0] || x > p[1]) ? -INFINITY : p[2];
+        case RVK_PRIOR_ECC_UNIFORM:
+            return (x < 0.0 || x >= p[0]) ? -INFINITY : p[1];
+        case RVK_PRIOR_NORMAL: {
+            const double y = (x - p[0]) / p[1];
+            return -0.5 * (y * y) - p[2];
+        }
+        case RVK_PRIOR_TRUNCNORM: {                      // scipy truncnorm.logpdf inside the bounds
+            if (x < p[2] || x > p[3]) return -INFINITY;
+            const double y = (x - p[0]) / p[1];
+            return ((-(y * y) / 2.0 - p[4]) - p[5]) - p[6];
+        }
+        case RVK_PRIOR_HALFNORMAL:
+            if (x < 0.0) return -INFINITY;
+            return halfnorm_lp(x, p[0], p[1], p[2]);
+        case RVK_PRIOR_RAYLEIGH:
+            if (x < 0.0) return -INFINITY;
+            return rayleigh_lp(x, p[0], p[1]);
+        case RVK_PRIOR_VANEYLEN19: {                     // scipy 1.15 logsumexp([hn, ry], b=[1-f, f])
+            if (x < 0.0) return -INFINITY;
+            const double b0 = p[4], b1 = p[5];
+            double a0 = halfnorm_lp(x, p[0], p[1], p[6]), a1 = rayleigh_lp(x, p[2], p[3]);
+            if (b0 == 0.0) a0 = -INFINITY;
+            if (b1 == 0.0) a1 = -INFINITY;
+            const double amax = (isnan(a0) || isnan(a1)) ? NAN : fmax(a0, a1);
+            const bool m0 = a0 == amax, m1 = a1 == amax;
+            const double m = b0 * (m0 ? 1.0 : 0.0) + b1 * (m1 ? 1.0 : 0.0);
+            const double shift = isfinite(amax) ? amax : 0.0;
+            double sum = b0 * exp((m0 ? -INFINITY : a0) - shift) + b1 * exp((m1 ? -INFINITY : a1) - shift);
+            sum = (sum == 0.0) ? sum : sum / m;
+            return (log1p(sum) + log(m)) + amax;
+        }
+        case RVK_PRIOR_BETA: {                           // xlogy(a-1, x) + xlog1py(b-1, -x) - log B
+            if (x < 0.0 || x > 1.0) return -INFINITY;
+            const double am1 = p[0] - 1.0, bm1 = p[1] - 1.0;
+            const double t1 = (am1 == 0.0 && !isnan(x)) ? 0.0 : am1 * log(x);
+            const double t2 = (bm1 == 0.0 && !isnan(x)) ? 0.0 : bm1 * log1p(-x);
+            return (t1 + t2) - p[2];
+        }
+        default:
+            return NAN;
+    }
+}
+
+// ---- Philox4x32-10 (counter-based; Salmon et al. 2011) -------------------------------
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+// 53-bit uniform in [0, 1) from two words (numpy's construction)
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// Draws of one (step, half, walker-in-half).
+struct Draw {
+    long long s, c;     // active walker, complementary walker
+    double zu, au;
+};
+
+struct RngArgs {
+    const int32_t *set;   // [steps][2][H] or nullptr (Philox)
+    const double *zu;
+    const int32_t *rint;
+    const double *au;
+    uint64_t seed, step0;
+};
+
+__device__ __forceinline__ Draw draw(const RngArgs &r, int step, int half, long long j, long long H) {
+    Draw d;
+    if (r.set) {
+        const long long o = ((long long)step * 2 + half) * H + j;
+        const long long ob = ((long long)step * 2 + (1 - half)) * H;
+        d.s = r.set[o];
+        d.c = r.set[ob + r.rint[o]];
+        d.zu = r.zu[o];
+        d.au = r.au[o];
+    } else {
+        const uint64_t st = r.step0 + (uint64_t)step;
+        const uint2 key = make_uint2((uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+        const uint4 a = philox(make_uint4((uint32_t)j, (uint32_t)half, (uint32_t)st, (uint32_t)(st >> 32)), key);
+        const uint4 b = philox(make_uint4((uint32_t)j, (uint32_t)half | 2u, (uint32_t)st, (uint32_t)(st >> 32)), key);
+        d.s = (long long)half * H + j;
+        // complement index in [0, H): multiply-shift (bias <= H / 2^32)
+        d.c = (long long)(1 - half) * H + (long long)(((uint64_t)b.x * (uint64_t)H) >> 32);
+        d.zu = u53(a.x, a.y);
+        d.au = u53(a.z, a.w);
+    }
+    return d;
+}
+
+// Per-walker prologue, one wave per walker: x (n_free coordinates, in LDS `lx`)
+// -> full row (LDS `lf` and global `full`) and the log-prior, which is returned
+// in every lane.  Lanes work over columns, planets and prior slots; the slot
+// terms are then summed by one lane in the reference's key order (fit.py:3684-3691).
+struct PostWaveLds {
+    double x[kMaxPFullPad];
+    double f[kMaxPFullPad];
+    double def[5 * RVK_MAX_PLANETS];
+    double term[kMaxPFullPad];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+inline __device__ double post_row_wave(const PostDev &pd, PostWaveLds &L, double *__restrict__ full) {
+    const int lane = threadIdx.x & 63;
+    for (int c = lane; c < pd.p_full; c += 64) {
+        const int f = pd.colmap[c];
+        const double v = f >= 0 ? L.x[f] : pd.tmpl[c];
+        L.f[c] = v;
+        full[c] = v;
+    }
+    wave_lds_sync();
+    const int jit0 = 5 * pd.n_planets + pd.n_inst;
+    bool dead = false;
+    if (lane < pd.n_inst) dead = L.f[jit0 + lane] < 0.0;                         // fit.py:3465-3468
+    if (pd.convert && lane < pd.n_planets) {                                       // fit.py:3426-3444
+        double *dp = L.def + 5 * lane;
+        const bool ok = to_default_t<-1>(L.f + 5 * lane, dp[0], dp[1], dp[2], dp[3], dp[4], pd.par);
+        dead |= !ok;                                                                // ValueError -> -inf
+    }
+    wave_lds_sync();
+    for (int k = lane; k < pd.n_prior; k += 64) {
+        const PriorSlot &s = pd.slots[k];
+        const double v = s.src >= 0 ? L.f[s.src] : L.def[-s.src - 1];
+        L.term[k] = prior_lp(s, v);
+    }
+    wave_lds_sync();
+    dead = __builtin_amdgcn_ballot_w64(dead) != 0;
+    double lp = 0.0;
+    for (int k = 0; k < pd.n_prior; ++k) lp += L.term[k];                          // same order, every lane
+    if (!isfinite(lp)) dead = true;                                                 // fit.py:3481-3482
+    return dead ? -INFINITY : lp;
+}
+
+// The accept / reject of one stretch-move half-step, fused into the epilogue of the
+// log-likelihood kernel (include/rvk_post.h rvk_stretch_run).  The kernel's walker w
+// is the w-th proposal of the active half (rows, log-priors from propose_kernel).
+struct SampleArgs {
+    int D;                      // n_free
+    const double *q;            // [H][D] proposals
+    const double *fac;          // [H] (ndim - 1) log z
+    const double *au;           // [H] acceptance uniforms
+    const long long *sidx;      // [H] walker index of proposal w
+    double *x;                  // [W][D] walker state (in/out)
+    double *lp;                 // [W] its log-posterior (in/out)
+    long long *nacc;            // [W] or nullptr
+    double *chain;              // this step's [W][D] or nullptr
+    double *lnpc;               // this step's [W] or nullptr
+    int *status;                // |= 1 on a NaN log-posterior
+};
+
+
+}  // namespace rvk

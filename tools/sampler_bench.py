@@ -1,0 +1,76 @@
+"""Stretch-move steps/s on BASELINE config 2 (1 planet, 256 epochs, W walkers):
+host sampler (numpy stretch move + LogPosterior.log_probability_batch, likelihood on the GPU)
+vs the device-resident sampler (rvk_stretch_run) with device (Philox) and host (emcee) draws.
+
+usage: python tools/sampler_bench.py [W=4096] [steps=200]
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+
+def build(W):
+    from ravest_amd import prior as P
+    from ravest_amd.posterior import LogPosterior
+    from ravest_amd.synth import make_config
+    ds = make_config(2, n_walkers=W)
+    free = [n for n in ds.names if n not in ("gd", "gdd")]
+    fixed = {"gd": 0.0, "gdd": 0.0}
+    priors = {}
+    for n in free:
+        v = ds.truth[n]
+        base = n.split("_")[0]
+        if base == "e":
+            priors[n] = P.EccentricityUniform(0.99)
+        elif base == "w":
+            priors[n] = P.Uniform(-np.pi, np.pi)
+        elif base == "jit":
+            priors[n] = P.HalfNormal(5.0)
+        else:
+            priors[n] = P.Uniform(v - 0.5 * abs(v) - 1.0, v + 0.5 * abs(v) + 1.0)
+    lpost = LogPosterior(ds.planet_letters, ds.parameterisation, priors, fixed, free, ds.time, ds.vel, ds.velerr,
+                         ds.instrument, ds.unique_instruments, ds.t0, device=0)
+    rng = np.random.default_rng(0)
+    x0 = np.array([ds.truth[n] for n in free])[None, :] * (1 + 1e-4 * rng.standard_normal((W, len(free))))
+    return lpost, x0
+
+
+def main():
+    import torch
+    from ravest_amd.sampler import DeviceEnsembleSampler, EnsembleSampler
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+    modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["host", "philox", "emcee"]
+    lpost, x0 = build(W)
+    D = x0.shape[1]
+    out = {"config": f"config 2 posterior: 1 planet, 256 epochs, {W} walkers, {D} free parameters", "steps": steps}
+
+    if "host" in modes:
+        s = EnsembleSampler(W, D, lpost.log_probability_batch, seed=1)
+        s.run_mcmc(x0, 5)
+        t = time.perf_counter()
+        s.run_mcmc(x0, steps)
+        out["host_sampler_ms_per_step"] = (time.perf_counter() - t) / steps * 1e3
+        out["host_sampler_acceptance"] = float(s.acceptance_fraction.mean())
+
+    for rng in [m for m in modes if m in ("philox", "emcee")]:
+        d = DeviceEnsembleSampler(lpost, W, seed=1 if rng == "philox" else np.random.RandomState(1), rng=rng,
+                                  steps_per_call=min(steps, 256))
+        d.run_mcmc(x0, 5)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        d.run_mcmc(x0, steps)
+        torch.cuda.synchronize()
+        out[f"device_{rng}_ms_per_step"] = (time.perf_counter() - t) / steps * 1e3
+        out[f"device_{rng}_acceptance"] = float(d.acceptance_fraction.mean())
+    if "host_sampler_ms_per_step" in out and "device_philox_ms_per_step" in out:
+        out["speedup_device_philox_vs_host"] = out["host_sampler_ms_per_step"] / out["device_philox_ms_per_step"]
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
