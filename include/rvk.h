@@ -105,8 +105,12 @@ int rvk_predict_device(rvk_handle *h, const double *d_theta, int64_t n_samples, 
 int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, double *sinE,
                      int32_t device, int32_t solver);
 
-/* Options. RVK_OPT_SOLVER: 0 = production solver (default), 1 = reference Halley. */
+/* Options. RVK_OPT_SOLVER: 0 = production solver (default), 1 = reference Halley.
+ * RVK_OPT_GRAPH: 0 (default) = rvk_stretch_run issues plain stream launches;
+ * 1 = it replays a cached HIP graph of 8 steps (same kernels; measured equal on
+ * MI355X at 4096 walkers, kept for launch-bound hosts). */
 #define RVK_OPT_SOLVER 1
+#define RVK_OPT_GRAPH  2
 int rvk_set_option(rvk_handle *h, int32_t key, int32_t value);
 
 /* Stream the handle uses (hipStream_t as void*). */

@@ -23,6 +23,7 @@ EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rv
            "rvk_stretch_run"]
 
 OPT_SOLVER = 1
+OPT_GRAPH = 2
 
 PRED_TREND = 0x0100
 PRED_GAMMA = 0x0200

@@ -179,24 +179,27 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
             }
             if constexpr (SAMPLE) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
+                const RunArgs &run = *sa.run;
                 const int D = sa.D;
                 const long long sw = sa.sidx[w];
-                const double lp_old = sa.lp[sw];
+                const double lp_old = run.lp[sw];
                 const bool acc = sa.fac[w] + res - lp_old > log(sa.au[w]);
-                double *xs = sa.x + sw * D;
+                double *xs = run.x + sw * D;
                 const double *qw = sa.q + w * D;
-                if (lane == 0 && isnan(res)) atomicOr(sa.status, 1);
+                const long long W2 = 2 * n_walkers;
+                double *chain = run.chain ? run.chain + (long long)sa.step * W2 * D : nullptr;
+                if (lane == 0 && isnan(res)) atomicOr(run.status, 1);
                 for (int c = lane; c < D; c += 64) {
                     const double v = acc ? qw[c] : xs[c];
                     if (acc) xs[c] = v;
-                    if (sa.chain) sa.chain[sw * D + c] = v;
+                    if (chain) chain[sw * D + c] = v;
                 }
                 if (lane == 0) {
                     if (acc) {
-                        sa.lp[sw] = res;
-                        if (sa.nacc) sa.nacc[sw] += 1;
+                        run.lp[sw] = res;
+                        if (run.nacc) run.nacc[sw] += 1;
                     }
-                    if (sa.lnpc) sa.lnpc[sw] = acc ? res : lp_old;
+                    if (run.lnpc) run.lnpc[(long long)sa.step * W2 + sw] = acc ? res : lp_old;
                 }
             } else {
                 if (lane == 0) out[w] = res;
@@ -497,6 +500,11 @@ int rvk_set_option(rvk_handle *h, int32_t key, int32_t value) {
         if (value != 0 && value != 1) return fail(RVK_E_ARG, "solver must be 0 (fast) or 1 (reference Halley)");
         h->solver = value;
         h->launch = pick_ll(h->n_planets, h->n_inst > 1, value, h->par == RVK_PAR_PKEWTP);
+        return RVK_OK;
+    }
+    if (key == RVK_OPT_GRAPH) {
+        if (value != 0 && value != 1) return fail(RVK_E_ARG, "graph must be 0 or 1");
+        h->graph = value;
         return RVK_OK;
     }
     return fail(RVK_E_ARG, "unknown option key");

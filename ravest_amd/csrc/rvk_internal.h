@@ -70,6 +70,7 @@ struct rvk_handle {
     rvk::loglike_launch_t launch = nullptr;
     rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
     int solver = 0;
+    int graph = 0;                           // RVK_OPT_GRAPH
 
     rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par}; }
     int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }

@@ -41,17 +41,19 @@ __global__ __launch_bounds__(256) void logprior_kernel(PostDev pd, const double 
 // proposal: q = c - (c - s) * z, z = ((a - 1) u + 1)^2 / a, factor = (ndim - 1) log z;
 // then its full row and log-prior.  The accept / reject runs in the epilogue of the
 // log-likelihood kernel (SAMPLE mode) or in accept_kernel.
-__global__ __launch_bounds__(256) void propose_kernel(PostDev pd, RngArgs rng, int step, int half, long long H,
-                                                      double a, const double *__restrict__ x,
-                                                      double *__restrict__ q, double *__restrict__ full,
+__global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs *__restrict__ runp, int step,
+                                                      int half, long long H, double *__restrict__ q,
+                                                      double *__restrict__ full,
                                                       double *__restrict__ lp, double *__restrict__ fac,
                                                       double *__restrict__ au, long long *__restrict__ sidx) {
     __shared__ PostWaveLds lds[kWavesPerBlock];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PostWaveLds &L = lds[wv];
     const int D = pd.n_free;
+    const RunArgs &run = *runp;
+    const double *x = run.x, a = run.a;
     for (long long j = (long long)blockIdx.x * kWavesPerBlock + wv; j < H; j += (long long)gridDim.x * kWavesPerBlock) {
-        const Draw d = draw(rng, step, half, j, H);
+        const Draw d = draw(run, step, half, j, H);
         const double zt = (a - 1.0) * d.zu + 1.0;
         const double z = zt * zt / a;
         const double *xs = x + d.s * D, *xc = x + d.c * D;
@@ -74,31 +76,34 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, RngArgs rng, i
 
 // Accept / reject (RedBlueMove.propose + update) and the chain write of the half, for the
 // unfused path (reference solver): one thread per proposal.
-__global__ __launch_bounds__(256) void accept_kernel(long long H, int D, const double *__restrict__ q,
-                                                     const double *__restrict__ fac, const double *__restrict__ au,
+__global__ __launch_bounds__(256) void accept_kernel(const RunArgs *__restrict__ runp, int step, long long H, int D,
+                                                     const double *__restrict__ q, const double *__restrict__ fac,
+                                                     const double *__restrict__ au,
                                                      const long long *__restrict__ sidx,
-                                                     const double *__restrict__ nlp_all, double *__restrict__ x,
-                                                     double *__restrict__ lp, long long *__restrict__ nacc,
-                                                     double *__restrict__ chain, double *__restrict__ lnpc,
-                                                     int *__restrict__ status) {
+                                                     const double *__restrict__ nlp_all) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= H) return;
+    const RunArgs &run = *runp;
     const long long s = sidx[j];
     const double nlp = nlp_all[j];
-    if (isnan(nlp)) atomicOr(status, 1);
-    const double lnpdiff = fac[j] + nlp - lp[s];
-    double *xs = x + s * D;
+    if (isnan(nlp)) atomicOr(run.status, 1);
+    const double lnpdiff = fac[j] + nlp - run.lp[s];
+    double *xs = run.x + s * D;
     if (lnpdiff > log(au[j])) {
         for (int k = 0; k < D; ++k) xs[k] = q[j * D + k];
-        lp[s] = nlp;
-        if (nacc) nacc[s] += 1;
+        run.lp[s] = nlp;
+        if (run.nacc) run.nacc[s] += 1;
     }
-    if (chain)
-        for (int k = 0; k < D; ++k) chain[s * D + k] = xs[k];
-    if (lnpc) lnpc[s] = lp[s];
+    if (run.chain)
+        for (int k = 0; k < D; ++k) run.chain[((long long)step * 2 * H + s) * D + k] = xs[k];
+    if (run.lnpc) run.lnpc[(long long)step * 2 * H + s] = run.lp[s];
 }
 
+__global__ void set_run_kernel(RunArgs *dst, RunArgs v) { *dst = v; }
+
 unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
+
+constexpr int kStepsPerGraph = 8;   // steps per cached graph replay (4 or 6 kernels each)
 
 // one wave per item, at most 2^16 blocks (grid-stride beyond)
 unsigned wave_blocks(long long n) {
@@ -117,15 +122,64 @@ struct rvk_post {
     double *d_tmpl = nullptr;
     PriorSlot *d_slots = nullptr;
     // workspace, sized for cap walkers
-    long long cap = 0;
+    long long capw = 0;
     double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_au = nullptr;
     long long *d_sidx = nullptr;
+    RunArgs *d_run = nullptr;              // rvk_stretch_run's per-chunk arguments
+    hipStream_t cap = nullptr;             // capture stream
+    hipGraphExec_t graph = nullptr;        // cached kStepsPerGraph-step chunk
+    long long graph_H = 0;
+    int graph_solver = -1;
 
     PostDev dev() const {
         return PostDev{n_free, h->p_full(), n_prior, h->n_planets, h->n_inst, h->par, convert, d_colmap, d_tmpl,
                        d_slots};
     }
 };
+
+// Kernels of n steps reading this chunk's RunArgs (p->d_run): propose, then the
+// likelihood with the accept / reject fused in (production solver) or the
+// likelihood and accept_kernel (reference solver).
+static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
+    rvk_handle *h = p->h;
+    const PostDev pd = p->dev();
+    const PostArgs post{p->d_lp, p->jac, p->renorm};
+    for (int s = 0; s < n; ++s)
+        for (int half = 0; half < 2; ++half) {
+            hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, s, half, H,
+                               p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
+            if (h->solver == 0 && h->sample) {
+                const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s};
+                h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
+            } else {
+                h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
+                hipLaunchKernelGGL(accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, p->d_run, s, H, p->n_free,
+                                   p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_nlp);
+            }
+        }
+}
+
+// The kStepsPerGraph-step chunk as a HIP graph, captured once per (H, solver) and
+// replayed: its kernel arguments never change (everything per call is in d_run).
+static int ensure_graph(rvk_post *p, long long H) {
+    if (p->graph && p->graph_H == H && p->graph_solver == p->h->solver) return RVK_OK;
+    if (p->graph) (void)hipGraphExecDestroy(p->graph);
+    p->graph = nullptr;
+    if (!p->cap) HIPCHK(hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking));
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(p->cap, hipStreamCaptureModeRelaxed));
+    enqueue_steps(p, p->cap, H, kStepsPerGraph);
+    HIPCHK(hipStreamEndCapture(p->cap, &g));
+    const hipError_t e = hipGraphInstantiate(&p->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        p->graph = nullptr;
+        return fail(RVK_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    }
+    p->graph_H = H;
+    p->graph_solver = p->h->solver;
+    return RVK_OK;
+}
 
 static void free_post(rvk_post *p) {
     if (!p) return;
@@ -140,11 +194,16 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_nlp);
     (void)hipFree(p->d_au);
     (void)hipFree(p->d_sidx);
+    (void)hipFree(p->d_run);
+    if (p->graph) (void)hipGraphExecDestroy(p->graph);
+    if (p->cap) (void)hipStreamDestroy(p->cap);
     delete p;
 }
 
 static int reserve_impl(rvk_post *p, long long W) {
-    if (W <= p->cap) return RVK_OK;
+    if (W <= p->capw) return RVK_OK;
+    if (p->graph) (void)hipGraphExecDestroy(p->graph);   // it holds the old workspace pointers
+    p->graph = nullptr;
     HIPCHK(hipSetDevice(p->h->device));
     (void)hipFree(p->d_full);
     (void)hipFree(p->d_lp);
@@ -155,7 +214,7 @@ static int reserve_impl(rvk_post *p, long long W) {
     (void)hipFree(p->d_sidx);
     p->d_full = p->d_lp = p->d_q = p->d_fac = p->d_nlp = p->d_au = nullptr;
     p->d_sidx = nullptr;
-    p->cap = 0;
+    p->capw = 0;
     const size_t w = (size_t)W;
     HIPCHK(hipMalloc(&p->d_full, sizeof(double) * w * (size_t)p->h->p_full()));
     HIPCHK(hipMalloc(&p->d_lp, sizeof(double) * w));
@@ -164,7 +223,7 @@ static int reserve_impl(rvk_post *p, long long W) {
     HIPCHK(hipMalloc(&p->d_nlp, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_au, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * w));
-    p->cap = W;
+    p->capw = W;
     return RVK_OK;
 }
 
@@ -204,6 +263,7 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
     HIPCHK(hipMalloc(&p->d_colmap, sizeof(int32_t) * pf));
     HIPCHK(hipMalloc(&p->d_tmpl, sizeof(double) * pf));
     HIPCHK(hipMalloc(&p->d_slots, sizeof(PriorSlot) * (n_prior > 0 ? n_prior : 1)));
+    HIPCHK(hipMalloc(&p->d_run, sizeof(RunArgs)));
     HIPCHK(hipMemcpy(p->d_colmap, colmap.data(), sizeof(int32_t) * pf, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(p->d_tmpl, tmpl, sizeof(double) * pf, hipMemcpyHostToDevice));
     if (n_prior > 0)
@@ -297,26 +357,31 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
     rvk_handle *h = p->h;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
-    const RngArgs rng{d_set, d_zu, d_rint, d_au, seed, step0};
-    const PostDev pd = p->dev();
-    const int D = p->n_free;
-    for (int s = 0; s < n_steps; ++s) {
-        double *ch = d_chain ? d_chain + (size_t)s * (size_t)W * (size_t)D : nullptr;
-        double *lc = d_lnp ? d_lnp + (size_t)s * (size_t)W : nullptr;
-        for (int half = 0; half < 2; ++half) {
-            hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, rng, s, half, H, a, d_x,
-                               p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
-            const PostArgs post{p->d_lp, p->jac, p->renorm};
-            if (h->solver == 0 && h->sample) {   // accept / reject fused into the likelihood kernel
-                const SampleArgs sa{D, p->d_q, p->d_fac, p->d_au, p->d_sidx, d_x, d_lp, (long long *)d_naccepted,
-                                    ch, lc, (int *)d_status};
-                h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
-            } else {
-                h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
-                hipLaunchKernelGGL(accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, H, D, p->d_q, p->d_fac,
-                                   p->d_au, p->d_sidx, p->d_nlp, d_x, d_lp, (long long *)d_naccepted, ch, lc,
-                                   (int *)d_status);
-            }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(st, &cs));
+    const bool use_graph = h->graph && cs == hipStreamCaptureStatusNone;   // a caller's capture records the launches
+    const size_t wd = (size_t)W * (size_t)p->n_free, hh = 2 * (size_t)H;
+    for (int s0 = 0; s0 < n_steps; s0 += kStepsPerGraph) {
+        const int n = (n_steps - s0) < kStepsPerGraph ? (n_steps - s0) : kStepsPerGraph;
+        RunArgs run{d_x,
+                    d_lp,
+                    (long long *)d_naccepted,
+                    (int *)d_status,
+                    d_chain ? d_chain + (size_t)s0 * wd : nullptr,
+                    d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
+                    d_set ? d_set + (size_t)s0 * hh : nullptr,
+                    d_set ? d_zu + (size_t)s0 * hh : nullptr,
+                    d_set ? d_rint + (size_t)s0 * hh : nullptr,
+                    d_set ? d_au + (size_t)s0 * hh : nullptr,
+                    seed,
+                    step0 + (uint64_t)s0,
+                    a};
+        hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+        if (use_graph && n == kStepsPerGraph) {
+            if ((rc = ensure_graph(p, H))) return rc;
+            HIPCHK(hipGraphLaunch(p->graph, st));
+        } else {
+            enqueue_steps(p, st, H, n);
         }
     }
     HIPCHK(hipGetLastError());

@@ -112,15 +112,25 @@ struct Draw {
     double zu, au;
 };
 
-struct RngArgs {
-    const int32_t *set;   // [steps][2][H] or nullptr (Philox)
+// Per-call arguments of rvk_stretch_run, kept in device memory (written by a one-thread
+// kernel at the start of each chunk of steps) so that the kernels of a chunk have
+// call-invariant arguments and can be replayed from a cached HIP graph.
+struct RunArgs {
+    double *x;            // [W][D] walker state (in/out)
+    double *lp;           // [W]
+    long long *nacc;      // [W] or nullptr
+    int *status;
+    double *chain;        // this chunk's first step [W][D] or nullptr
+    double *lnpc;         // this chunk's first step [W] or nullptr
+    const int32_t *set;   // host draws for this chunk's steps [step][2][H], or nullptr (Philox)
     const double *zu;
     const int32_t *rint;
     const double *au;
-    uint64_t seed, step0;
+    uint64_t seed, step0; // Philox key, global step of the chunk's first step
+    double a;
 };
 
-__device__ __forceinline__ Draw draw(const RngArgs &r, int step, int half, long long j, long long H) {
+__device__ __forceinline__ Draw draw(const RunArgs &r, int step, int half, long long j, long long H) {
     Draw d;
     if (r.set) {
         const long long o = ((long long)step * 2 + half) * H + j;
@@ -200,13 +210,8 @@ struct SampleArgs {
     const double *fac;          // [H] (ndim - 1) log z
     const double *au;           // [H] acceptance uniforms
     const long long *sidx;      // [H] walker index of proposal w
-    double *x;                  // [W][D] walker state (in/out)
-    double *lp;                 // [W] its log-posterior (in/out)
-    long long *nacc;            // [W] or nullptr
-    double *chain;              // this step's [W][D] or nullptr
-    double *lnpc;               // this step's [W] or nullptr
-    int *status;                // |= 1 on a NaN log-posterior
+    const RunArgs *run;         // state, chain and status pointers
+    int step;                   // step within the chunk
 };
-
 
 }  // namespace rvk
