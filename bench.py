@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--walkers", type=int, default=None, help="walkers per GPU (default: config's, 4096 for cfg 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sampler", action="store_true", help="skip the device stretch-move measurement")
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
     ap.add_argument("--streams", type=int, default=1, help="independent streams per graph")
     return ap.parse_args()
@@ -84,6 +85,52 @@ def load_pmc(cfg):
         with open(p) as f:
             return json.load(f)
     return None
+
+
+def sampler_line(W: int, steps: int = 256) -> dict:
+    """Device-resident stretch move (rvk_stretch_run) on the config-2
+    posterior: ms per emcee step of W walkers (both halves: proposals, priors, likelihood,
+    accept/reject, chain write into HBM), HIP events on the launch stream; next to the host
+    stretch move driving the same posterior (numpy + LogPosterior.log_probability_batch)."""
+    import torch
+    from ravest_amd import _lib
+    from ravest_amd.posterior import DevicePosterior
+    from ravest_amd.sampler import EnsembleSampler
+    from ravest_amd.synth import make_posterior
+    lpost, x0 = make_posterior(2, W, device=torch.cuda.current_device())
+    D = x0.shape[1]
+    dp = DevicePosterior(lpost)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    x = torch.from_numpy(x0).to(dev)
+    lp = torch.empty(W, dtype=torch.float64, device=dev)
+    dp.device(x, lp)
+    chain = torch.empty((steps, W, D), dtype=torch.float64, device=dev)
+    lnpc = torch.empty((steps, W), dtype=torch.float64, device=dev)
+    nacc = torch.zeros(W, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    L = _lib.load()
+    st = torch.cuda.current_stream(dev)
+
+    def run(n, step0):
+        _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, 1234, step0, 0, 0, 0, 0,
+                                     chain.data_ptr(), lnpc.data_ptr(), nacc.data_ptr(), status.data_ptr(),
+                                     st.cuda_stream))
+    run(16, 0)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    run(steps, 16)
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    dev_ms = a.elapsed_time(b) / steps
+    acc = float(nacc.sum().item()) / ((steps + 16) * W)
+    hs = EnsembleSampler(W, D, lpost.log_probability_batch, seed=1)
+    hs.run_mcmc(x0, 2)
+    t0 = time.perf_counter()
+    hs.run_mcmc(x0, 20)
+    host_ms = (time.perf_counter() - t0) / 20 * 1e3
+    return {"what": f"device stretch move (rvk_stretch_run), config-2 posterior, {W} walkers, {D} free parameters, "
+                    "Philox draws, chain in HBM", "ms_per_step": dev_ms, "walker_steps_per_s": W / (dev_ms * 1e-3),
+            "acceptance": acc, "host_stretch_move_ms_per_step": host_ms, "speedup_vs_host": host_ms / dev_ms}
 
 
 def main():
@@ -260,6 +307,8 @@ def main():
             "valu": valu,
         }
         line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
+        if world == 1 and not args.no_sampler:
+            line["sampler"] = sampler_line(W)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -37,6 +37,12 @@ namespace {
 #ifndef RVK_TAB_LDS
 #define RVK_TAB_LDS 1                 // sin/cos table staged in LDS (1) or read through L1 (0)
 #endif
+#ifndef RVK_PREP_TAB
+#define RVK_PREP_TAB 1                // prep's sin/cos(w) from the LDS table (1) or fdlibm (0)
+#endif
+#ifndef RVK_TP_INLINE
+#define RVK_TP_INLINE 1               // "P K e w Tp": inline conversion in the prep (1) or the out-of-line one (0)
+#endif
 #ifndef RVK_LB_WAVES
 #define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             const double *p5 = theta + w * stride + 5 * p;
             PlanetK pk;
             // "P K e w Tp" inline (no call, no scratch); the others out of line
-            const bool ok = TP ? planet_consts_t<0>(p5, pk) : planet_consts(d.par, p5, pk);
+            const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
             pks[j][p] = pk;
             okp[j][p] = ok;
         }
@@ -169,11 +175,10 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             };
             if ((gd != 0.0) | (gdd != 0.0)) epochs(std::true_type{});
             else epochs(std::false_type{});
+            // prod is a frexp mantissa in [0.5, 1) unless the product hit 0 (some s^2 = 0), inf or NaN,
+            // whose log is -inf, inf, NaN whatever the exponent
             double lsum = log_frexp(prod, expo);
-            const bool special = !(prod >= 0.5 && prod < 1.0);   // a product of 0, inf or NaN
-            if (__builtin_amdgcn_ballot_w64(special)) {          // rare: keep the generic log off the common path
-                if (special) lsum = log(prod) + (double)expo * kLn2;
-            }
+            if (!(prod >= 0.5 && prod < 1.0)) lsum = prod == 0.0 ? -INFINITY : prod;
             double tot = wave_sum(chi2 + lsum);
             res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
             if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
@@ -455,8 +460,8 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->n_planets = n_planets;
     h->par = par;
     h->t0 = t0;
-    h->launch = pick_ll(n_planets, n_inst > 1, 0, par == RVK_PAR_PKEWTP);
-    h->sample = pick_sample(n_planets, n_inst > 1, par == RVK_PAR_PKEWTP);
+    h->launch = pick_ll(n_planets, n_inst > 1, 0, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample = pick_sample(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;
@@ -499,7 +504,7 @@ int rvk_set_option(rvk_handle *h, int32_t key, int32_t value) {
     if (key == RVK_OPT_SOLVER) {
         if (value != 0 && value != 1) return fail(RVK_E_ARG, "solver must be 0 (fast) or 1 (reference Halley)");
         h->solver = value;
-        h->launch = pick_ll(h->n_planets, h->n_inst > 1, value, h->par == RVK_PAR_PKEWTP);
+        h->launch = pick_ll(h->n_planets, h->n_inst > 1, value, RVK_TP_INLINE && h->par == RVK_PAR_PKEWTP);
         return RVK_OK;
     }
     if (key == RVK_OPT_GRAPH) {

@@ -383,8 +383,12 @@ __device__ __forceinline__ bool to_default_t(const double *p5, double &P, double
     return ok;
 }
 
-template <int PAR>
-__device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, int par = PAR) {
+// TAB: sin/cos(w) from the LDS table `tab` (w is in [-pi, pi) for a valid planet;
+// an invalid one is masked and w = 0 is used), sharing the epoch loop's constants
+// instead of holding fdlibm's coefficients for the prep alone.
+template <int PAR, bool TAB = false>
+__device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, int par = PAR,
+                                                const SC *tab = nullptr) {
     double P, K, e, w, Tp;
     bool ok = to_default_t<PAR>(p5, P, K, e, w, Tp, par);
     ok = ok && valid_default(P, K, e, w);
@@ -395,7 +399,8 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
     pk.Tp = Tp;
     pk.e = e;
     double sw, cw;
-    sincos_mod(w, sw, cw);
+    if (TAB) sincos_tab(w, tab, sw, cw);
+    else sincos_mod(w, sw, cw);
     pk.K = K;
     pk.cw = cw;
     pk.sqsw = sqrt(1.0 - e * e) * sw;

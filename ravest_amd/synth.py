@@ -151,3 +151,32 @@ def make_config(cfg: int, n_walkers: int | None = None) -> Dataset:
     ds = make_dataset(c["n_planets"], c["n_epochs"], c["n_inst"], seed=c["seed"])
     ds.theta = make_walkers(ds, n_walkers or c["n_walkers"], seed=c["seed"])
     return ds
+
+
+def make_posterior(config: int = 2, n_walkers: int | None = None, device: int = -1, seed: int = 0):
+    """A LogPosterior over the config's synthetic dataset with built-in priors on every
+    free parameter (trend fixed at 0), and a tight starting ball around the truth.
+    Used by the sampler benchmarks (bench.py "sampler", tools/sampler_bench.py)."""
+    from . import prior as P
+    from .posterior import LogPosterior
+    ds = make_config(config, n_walkers=n_walkers or 8)
+    free = [n for n in ds.names if n not in ("gd", "gdd")]
+    fixed = {"gd": 0.0, "gdd": 0.0}
+    priors = {}
+    for n in free:
+        v = ds.truth[n]
+        base = n.split("_")[0]
+        if base == "e":
+            priors[n] = P.EccentricityUniform(0.99)
+        elif base == "w":
+            priors[n] = P.Uniform(-np.pi, np.pi)
+        elif base == "jit":
+            priors[n] = P.HalfNormal(5.0)
+        else:
+            priors[n] = P.Uniform(v - 0.5 * abs(v) - 1.0, v + 0.5 * abs(v) + 1.0)
+    lpost = LogPosterior(ds.planet_letters, ds.parameterisation, priors, fixed, free, ds.time, ds.vel, ds.velerr,
+                         ds.instrument, ds.unique_instruments, ds.t0, device=device)
+    W = n_walkers or CONFIGS[config]["n_walkers"]
+    rng = np.random.default_rng(seed)
+    x0 = np.array([ds.truth[n] for n in free])[None, :] * (1 + 1e-4 * rng.standard_normal((W, len(free))))
+    return lpost, x0

@@ -5,19 +5,28 @@ import numpy as np, torch
 from ravest_amd.engine import RVEngine
 from ravest_amd.synth import make_config, make_dataset, make_walkers
 
-def timeit(eng, th, out, reps=30, rounds=5):
-    s = torch.cuda.current_stream()
-    for _ in range(5):
-        eng.loglike_device(th, out, s)
+def timeit(eng, th, out, reps=20, rounds=7, G=20):
+    """us per launch: HIP events around replays of a G-launch HIP graph (as bench.py), median of rounds."""
+    cap = torch.cuda.Stream()
+    for _ in range(3):
+        eng.loglike_device(th, out, cap)
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        for _ in range(G):
+            eng.loglike_device(th, out, cap)
+    g.replay()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
     res = []
     for r in range(rounds):
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
         for a, b in evs:
-            a.record(s); eng.loglike_device(th, out, s); b.record(s)
+            a.record(s); g.replay(); b.record(s)
         torch.cuda.synchronize()
-        res.append(np.median([a.elapsed_time(b) for a, b in evs]))
+        res.append(np.median([a.elapsed_time(b) for a, b in evs]) / G)
     return float(np.median(res)) * 1e3  # us
+
 
 def main():
     from ravest_amd import _lib

@@ -14,7 +14,7 @@ kname = None
 for f in sorted(glob.glob(os.path.join(out_dir, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for row in csv.DictReader(open(f)):
         name = row.get("Kernel_Name", "")
-        if "loglike_kernel" not in name:
+        if "loglike_kernel<" not in name or ", false>(" not in name:   # the plain (non-sampler) launch
             continue
         kname = name
         c = row["Counter_Name"]
@@ -22,7 +22,7 @@ for f in sorted(glob.glob(os.path.join(out_dir, "p*", "**", "*counter_collection
         disp[c].add(row.get("Dispatch_Id", row.get("Correlation_Id")))
 per = {c: vals[c] / max(1, len(disp[c])) for c in vals}
 res = {"kernel": kname, "counters_per_launch": per,
-       "source": f"rocprofv3 --pmc passes over `python bench.py --config {cfg} --steps 20 --warmup 5` (tools/pmc.sh)"}
+       "source": f"rocprofv3 --pmc passes over `python bench.py --config {cfg} --steps 20 --warmup 5 --no-cpu-baseline --no-sampler` (tools/pmc.sh)"}
 if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     res["hbm_bytes_per_launch"] = (2 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
 if "SQ_INSTS_VALU" in per:

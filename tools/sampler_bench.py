@@ -14,29 +14,8 @@ import numpy as np  # noqa: E402
 
 
 def build(W):
-    from ravest_amd import prior as P
-    from ravest_amd.posterior import LogPosterior
-    from ravest_amd.synth import make_config
-    ds = make_config(2, n_walkers=W)
-    free = [n for n in ds.names if n not in ("gd", "gdd")]
-    fixed = {"gd": 0.0, "gdd": 0.0}
-    priors = {}
-    for n in free:
-        v = ds.truth[n]
-        base = n.split("_")[0]
-        if base == "e":
-            priors[n] = P.EccentricityUniform(0.99)
-        elif base == "w":
-            priors[n] = P.Uniform(-np.pi, np.pi)
-        elif base == "jit":
-            priors[n] = P.HalfNormal(5.0)
-        else:
-            priors[n] = P.Uniform(v - 0.5 * abs(v) - 1.0, v + 0.5 * abs(v) + 1.0)
-    lpost = LogPosterior(ds.planet_letters, ds.parameterisation, priors, fixed, free, ds.time, ds.vel, ds.velerr,
-                         ds.instrument, ds.unique_instruments, ds.t0, device=0)
-    rng = np.random.default_rng(0)
-    x0 = np.array([ds.truth[n] for n in free])[None, :] * (1 + 1e-4 * rng.standard_normal((W, len(free))))
-    return lpost, x0
+    from ravest_amd.synth import make_posterior
+    return make_posterior(2, W, device=0)
 
 
 def main():

@@ -1,13 +1,15 @@
 #!/bin/bash
-# Build A/B variants of librvk.so from the same source (different -D knobs).
+# Build A/B variants of librvk.so from the same source (different -D knobs):
+#   tools/variants.sh name1:"-DFOO=1" name2:"-DBAR=0" ...   (base = no flags is always built)
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p build/variants
+rm -rf build/variants && mkdir -p build/variants
 build() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
-  -o build/variants/librvk_$name.so ravest_amd/csrc/rvk.hip 2>/dev/null & }
+  -o build/variants/librvk_$name.so ravest_amd/csrc/rvk.hip ravest_amd/csrc/rvk_post.hip 2>/dev/null & }
 build base
-build abl1 -DRVK_ABLATE=1
-build abl2 -DRVK_ABLATE=2
-build abl3 -DRVK_ABLATE=3
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  build $name $flags
+done
 wait
 ls build/variants
