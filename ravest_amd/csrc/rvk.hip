@@ -37,6 +37,9 @@ namespace {
 #ifndef RVK_TAB_LDS
 #define RVK_TAB_LDS 1                 // sin/cos table staged in LDS (1) or read through L1 (0)
 #endif
+#ifndef RVK_UNROLL2
+#define RVK_UNROLL2 0                 // epoch loop: two epochs per trip, ping-pong prefetch registers (1)
+#endif
 #ifndef RVK_PREP_TAB
 #define RVK_PREP_TAB 1                // prep's sin/cos(w) from the LDS table (1) or fdlibm (0)
 #endif
@@ -135,31 +138,21 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             // common case carries no trend arithmetic at all.
             auto epochs = [&](auto trend_c) {
                 constexpr bool TREND = decltype(trend_c)::value;
-                // software pipeline: the next epoch's data is in flight during this epoch's solve
-                double tn = t_1, vn = v_1, sn = s_1;
-                int in_ = i_1;
-                for (int i = lane; i < n_epochs; i += 64) {
-                    const double t = tn, vel = vn, s2b = sn;
-                    const int ii = in_;
-                    const int inx = i + 64;
-                    if (inx < n_epochs) {
-                        tn = d.t[inx]; vn = d.vel[inx]; sn = d.s2[inx];
-                        if (MULTI) in_ = d.inst[inx];
-                    }
-                    double rv = 0.0;
-#pragma unroll
-                    for (int p = 0; p < NP; ++p) rv += planet_rv<SOLVER>(pk[p], t, tab);
-                    if (TREND) {
-                        const double dt = t - d.t0;
-                        rv += __builtin_fma(gd, dt, gdd * (dt * dt));
-                    }
+                // one epoch: gamma + planets (+ trend), chi^2 term, s^2 into the running product
+                auto one = [&](double t, double vel, double s2b, int ii) {
                     double gam = g0, jj = j0;
                     if (MULTI) {
                         for (int k = 1; k < n_inst; ++k) {
                             if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
                         }
                     }
-                    rv += gam;
+                    double rv = gam;   // each planet's K * (...) lands in one FMA
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) rv = planet_rv<SOLVER>(pk[p], t, tab, rv);
+                    if (TREND) {
+                        const double dt = t - d.t0;
+                        rv += __builtin_fma(gd, dt, gdd * (dt * dt));
+                    }
                     const double s2 = s2b + jj;
                     const double r = rv - vel;
 #if RVK_CHI_NR2
@@ -171,7 +164,38 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                     int ex;
                     prod = __builtin_frexp(prod, &ex);
                     expo += ex;
+                };
+                // Lane epochs i, i+64, ...  RVK_UNROLL2: two per trip with ping-pong registers
+                // (A, B), no register shuffling between trips; invariant: A holds epoch i.
+#if RVK_UNROLL2
+                double tA = t_1, vA = v_1, sA = s_1, tB = 0.0, vB = 0.0, sB = 1.0;
+                int iA = i_1, iB = 0;
+                int i = lane;
+                for (; i + 64 < n_epochs; i += 128) {
+                    tB = d.t[i + 64]; vB = d.vel[i + 64]; sB = d.s2[i + 64];
+                    if (MULTI) iB = d.inst[i + 64];
+                    one(tA, vA, sA, iA);
+                    if (i + 128 < n_epochs) {
+                        tA = d.t[i + 128]; vA = d.vel[i + 128]; sA = d.s2[i + 128];
+                        if (MULTI) iA = d.inst[i + 128];
+                    }
+                    one(tB, vB, sB, iB);
                 }
+                if (i < n_epochs) one(tA, vA, sA, iA);
+#else
+                // one epoch per trip; the next epoch's loads are issued before this one's solve
+                double tn = t_1, vn = v_1, sn = s_1;
+                int in_ = i_1;
+                for (int i = lane; i < n_epochs; i += 64) {
+                    const double t = tn, vel = vn, s2b = sn;
+                    const int ii = in_;
+                    if (i + 64 < n_epochs) {
+                        tn = d.t[i + 64]; vn = d.vel[i + 64]; sn = d.s2[i + 64];
+                        if (MULTI) in_ = d.inst[i + 64];
+                    }
+                    one(t, vel, s2b, ii);
+                }
+#endif
             };
             if ((gd != 0.0) | (gdd != 0.0)) epochs(std::true_type{});
             else epochs(std::false_type{});
@@ -244,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restric
             double v = 0.0;
             const double t = tq[j];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) v += planet_rv<SOLVER>(pk[p], t, tab);
+            for (int p = 0; p < NP; ++p) v = planet_rv<SOLVER>(pk[p], t, tab, v);
             if (what & RVK_PRED_TREND) {
                 const double dt = t - t0;
                 v += __builtin_fma(gd, dt, gdd * (dt * dt));

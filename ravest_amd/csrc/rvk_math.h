@@ -173,8 +173,8 @@ __device__ __forceinline__ void sincos_tab(double E, const SC *tab, double &S, d
     const double d = E - a;                      // exact (Sterbenz)
     const SC sc = tab[(int)jj + kTabHalf];
     const double z = d * d;
-    const double sd = __builtin_fma(d * z, fma_s(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
-    const double cm = z * __builtin_fma(z, fma_s(z, __builtin_fma(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
+    const double sd = __builtin_fma(d * z, fma_s(z, fma_s(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
+    const double cm = z * __builtin_fma(z, fma_s(z, fma_s(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
     S = __builtin_fma(sc.s, cm, __builtin_fma(sc.c, sd, sc.s));
     C = __builtin_fma(sc.c, cm, __builtin_fma(-sc.s, sd, sc.c));
 }
@@ -235,8 +235,12 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
     double E = (double)Ef, S, C;
     sincos_tab(E, tab, S, C);
     if (RVK_ABLATE & 1) { cosE = C; sinE = S; return; }
-#pragma unroll 1
-    for (int it = 0; it < 8; ++it) {
+#ifndef RVK_HH_SINGLE
+#define RVK_HH_SINGLE 1
+#endif
+    // One Householder (order 3) step from (E, S = sin E, C = cos E); returns the step d
+    // and leaves t ~ 1/den for the error estimate.
+    auto step = [&](double &t) -> double {
         const double f = E - e * S - r;
         const double f1 = 1.0 - e * C;
         const double f2 = e * S;
@@ -244,12 +248,11 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
         const double f11 = f1 * f1;
         const double num = f * __builtin_fma(-3.0 * f, f2, 6.0 * f11);                        // f (6 f1^2 - 3 f f2)
         const double den = __builtin_fma(f * f, f3, 6.0 * f1 * __builtin_fma(-f, f2, f11));  // 6f1^3 - 6 f f1 f2 + f^2 f3
-        double t = __builtin_amdgcn_rcp(den);
+        t = __builtin_amdgcn_rcp(den);
         t = __builtin_fma(t, __builtin_fma(-den, t, 1.0), t);
         const double d = -num * t;
         E += d;
-        const double ad = __builtin_fabs(d);
-        if (ad > 1e-4) {                   // too far for the short series: re-anchor on the table
+        if (__builtin_fabs(d) > 1e-4) {    // too far for the short series: re-anchor on the table
             sincos_tab(E, tab, S, C);
         } else {                           // |d| <= 1e-4: sin d = d - d^3/6 (+8e-23), cos d = 1 - d^2/2 (+4e-18)
             const double z = d * d;
@@ -260,16 +263,23 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
             S = Sn;
             C = Cn;
         }
-        // next error ~ (e/f1)^3 d^4.  For e <= 0.9, (e/f1)^3 <= 729, so |d| <= 1e-5 already
-        // bounds it by 7.3e-18 (one compare); otherwise estimate it as 6 e^3 d^4 / den.
-#ifndef RVK_HH_SINGLE
-#define RVK_HH_SINGLE 1
-#endif
-        if (RVK_HH_SINGLE && e <= 0.9) {
-            if (ad <= 1e-5) break;
-        } else {
-            const double z2 = (d * d) * (d * d);
-            if (z2 * e6e3 * __builtin_fabs(t) < 1e-17) break;
+        return d;
+    };
+    // next error ~ (e/f1)^3 d^4.  For e <= 0.9, (e/f1)^3 <= 729, so |d| <= 1e-5 already
+    // bounds it by 7.3e-18 (one compare); otherwise estimate it as 6 e^3 d^4 / den.
+    auto converged = [&](double d, double t) -> bool {
+        if (RVK_HH_SINGLE && e <= 0.9) return __builtin_fabs(d) <= 1e-5;
+        const double z2 = (d * d) * (d * d);
+        return z2 * e6e3 * __builtin_fabs(t) < 1e-17;
+    };
+    // the first step is peeled (no loop-carried register shuffles on the common one-step path)
+    double t;
+    double d = step(t);
+    if (!converged(d, t)) {
+#pragma unroll 1
+        for (int it = 1; it < 8; ++it) {
+            d = step(t);
+            if (converged(d, t)) break;
         }
     }
     cosE = C;
@@ -418,13 +428,17 @@ __device__ __attribute__((noinline)) bool planet_consts(int par, const double *p
 // One planet's RV at time t (model.py:327, 119-121, 170).  e == 0 takes the
 // same arithmetic (the solvers return E = M), so there is no branch.
 template <int SOLVER>
-__device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const SC *tab) {
+// acc + (this planet's RV at t).  1/(1 - e cos E) with one Newton step on v_rcp_f64
+// (<= 2.2e-15 relative, like the chi^2 terms); the divisor is in (0, 2).
+__device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const SC *tab, double acc) {
     const double M = pk.n * (t - pk.Tp);
     double cE, sE;
     if (SOLVER == 1) solve_kepler_ref(M, pk.e, cE, sE);
     else solve_kepler_fast(M, pk.e, pk.e6e3, tab, cE, sE);
-    const double inv = rcp_nr(1.0 - pk.e * cE);
-    return pk.K * __builtin_fma(inv, __builtin_fma(cE - pk.e, pk.cw, -sE * pk.sqsw), pk.ecw);
+    const double b = 1.0 - pk.e * cE;
+    double inv = __builtin_amdgcn_rcp(b);
+    inv = __builtin_fma(inv, __builtin_fma(-b, inv, 1.0), inv);
+    return __builtin_fma(pk.K, __builtin_fma(inv, __builtin_fma(cE - pk.e, pk.cw, -sE * pk.sqsw), pk.ecw), acc);
 }
 
 // Wave64 sum in a fixed order (bitwise reproducible): DPP butterflies inside each
