@@ -111,6 +111,10 @@ int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, 
  * MI355X at 4096 walkers, kept for launch-bound hosts). */
 #define RVK_OPT_SOLVER 1
 #define RVK_OPT_GRAPH  2
+/* RVK_OPT_LPW: lanes of a wave per walker for the log-likelihood kernel: 0 (default)
+ * = chosen per launch from (walkers, epochs); 64, 32 or 16 = forced.  Fewer lanes per
+ * walker share a wave's fixed costs between 2 or 4 walkers when epochs are few. */
+#define RVK_OPT_LPW    3
 int rvk_set_option(rvk_handle *h, int32_t key, int32_t value);
 
 /* Stream the handle uses (hipStream_t as void*). */

@@ -24,6 +24,7 @@ EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rv
 
 OPT_SOLVER = 1
 OPT_GRAPH = 2
+OPT_LPW = 3
 
 PRED_TREND = 0x0100
 PRED_GAMMA = 0x0200

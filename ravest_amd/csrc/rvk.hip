@@ -238,6 +238,126 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
     }
 }
 
+// Segmented variant: LPW lanes per walker, SEG = 64 / LPW walkers per wave (production
+// solver, no sampler epilogue).  For few epochs per walker the fixed costs of a wave
+// (constants, the per-walker setup, the log and the reduction) are shared by SEG walkers.
+// Per-walker values live in VGPRs (they differ between segments); the epoch loop is the
+// same, lanes stride their walker's epochs by LPW; each segment is summed with the row
+// butterflies and v_readlane of its rows.
+template <int NP, bool MULTI, bool TP, int LPW>
+__global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int n_epochs, int n_inst,
+                                                                 const double *__restrict__ theta,
+                                                                 long long n_walkers, long long stride, int wb,
+                                                                 double *__restrict__ out, PostArgs post) {
+    constexpr int SEG = 64 / LPW;
+    constexpr int WB = PassCfg<NP>::WB;
+    static_assert(WB % (kWavesPerBlock * SEG) == 0, "pass size must be a multiple of the block's walkers");
+    __shared__ PlanetK pks[WB][NP];
+    __shared__ int okp[WB][NP];
+    __shared__ SC tab[kTabN];
+    const int lane = threadIdx.x & 63, seg = lane / LPW, li = lane % LPW;
+    double t_1 = 0.0, v_1 = 0.0, s_1 = 1.0;
+    int i_1 = 0;
+    if (li < n_epochs) {
+        t_1 = d.t[li]; v_1 = d.vel[li]; s_1 = d.s2[li];
+        if (MULTI) i_1 = d.inst[li];
+    }
+    for (int i = threadIdx.x; i < kTabN; i += kBlock) tab[i] = d.tab[i];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
+        const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
+        for (int k = threadIdx.x; k < nb * NP; k += kBlock) {
+            const int j = k / NP, p = k - j * NP;
+            const double *p5 = theta + (base + j) * stride + 5 * p;
+            PlanetK pk;
+            const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
+            pks[j][p] = pk;
+            okp[j][p] = ok;
+        }
+        __syncthreads();
+        for (int j0 = wv * SEG; j0 < nb; j0 += kWavesPerBlock * SEG) {
+            const bool have = j0 + seg < nb;
+            const int j = have ? j0 + seg : j0;                  // this lane's walker slot
+            const long long w = base + j;
+            const double *row = theta + w * stride;
+            const double lpw = post.lp ? post.lp[w] : 0.0;
+            bool ok = have && lpw != -INFINITY;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) ok &= okp[j][p] != 0;
+            const double *g = row + 5 * NP;
+            const double *jit = g + n_inst;
+            const double gd = jit[n_inst], gdd = jit[n_inst + 1];
+            const double g0 = g[0], j0sq = jit[0] * jit[0];
+            PlanetK pk[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pk[p] = pks[j][p];
+            double chi2 = 0.0, prod = 0.5;
+            int expo = 1;
+            auto epochs = [&](auto trend_c) {
+                constexpr bool TREND = decltype(trend_c)::value;
+                double tn = t_1, vn = v_1, sn = s_1;
+                int in_ = i_1;
+                for (int i = li; i < n_epochs; i += LPW) {
+                    const double t = tn, vel = vn, s2b = sn;
+                    const int ii = in_;
+                    if (i + LPW < n_epochs) {
+                        tn = d.t[i + LPW]; vn = d.vel[i + LPW]; sn = d.s2[i + LPW];
+                        if (MULTI) in_ = d.inst[i + LPW];
+                    }
+                    double gam = g0, jj = j0sq;
+                    if (MULTI) {
+                        for (int k = 1; k < n_inst; ++k) {
+                            if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
+                        }
+                    }
+                    double rv = gam;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) rv = planet_rv<0>(pk[p], t, tab, rv);
+                    if (TREND) {
+                        const double dt = t - d.t0;
+                        rv += __builtin_fma(gd, dt, gdd * (dt * dt));
+                    }
+                    const double s2 = s2b + jj;
+                    const double r = rv - vel;
+                    chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);
+                    prod *= s2;
+                    int ex;
+                    prod = __builtin_frexp(prod, &ex);
+                    expo += ex;
+                }
+            };
+            if (ok) {
+                if (__builtin_amdgcn_ballot_w64((gd != 0.0) | (gdd != 0.0))) epochs(std::true_type{});
+                else epochs(std::false_type{});
+            }
+            double lsum = log_frexp(prod, expo);
+            if (!(prod >= 0.5 && prod < 1.0)) lsum = prod == 0.0 ? -INFINITY : prod;
+            const double v = row_sum(ok ? chi2 + lsum : 0.0);
+            const unsigned long long okm = __builtin_amdgcn_ballot_w64(ok);
+            // the segment totals are read (v_readlane) in uniform control flow: inside the
+            // lane-0 branch below the compiler may sink the last butterfly add into it, and
+            // the other rows' lanes would never compute it
+            double res[SEG];
+#pragma unroll
+            for (int k = 0; k < SEG; ++k) {
+                double tot = readlane_d(v, k * LPW);
+#pragma unroll
+                for (int r = 1; r < LPW / 16; ++r) tot += readlane_d(v, k * LPW + 16 * r);
+                res[k] = -0.5 * (tot + (double)n_epochs * kLog2Pi);
+                if (post.lp) res[k] = ((res[k] + readlane_d(lpw, k * LPW)) + post.jac) + post.renorm;
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < SEG; ++k) {
+                    if (j0 + k >= nb) break;
+                    out[base + j0 + k] = ((okm >> (k * LPW)) & 1ull) ? res[k] : -INFINITY;
+                }
+            }
+        }
+        if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();
+    }
+}
+
 // Posterior predictive (fit.py:2690-2939): one wave per sample, lanes over times.
 template <int NP, int SOLVER>
 __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restrict__ tq, const int32_t *__restrict__ iq,
@@ -316,9 +436,41 @@ void ll_grid(long long W, long long &blocks, int &wb) {
     }
 }
 
+template <int NP, bool MULTI, bool TP, int LPW>
+void launch_seg(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
+                double *out, PostArgs post) {
+    constexpr int SEG = 64 / LPW, PER = kWavesPerBlock * SEG, WB = PassCfg<NP>::WB;
+    long long blocks = (W + PER - 1) / PER;
+    int wb = PER;
+    if (blocks > kMaxBlocks) {
+        long long per = (W + kMaxBlocks - 1) / kMaxBlocks;
+        per = ((per + PER - 1) / PER) * PER;
+        wb = (int)(per < WB ? per : WB);
+        blocks = (W + wb - 1) / wb;
+        if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+    }
+    hipLaunchKernelGGL((loglike_seg_kernel<NP, MULTI, TP, LPW>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
+                       ni, th, W, stride, wb, out, post);
+}
+
+// Lanes per walker for a launch.  Measured on MI355X (tools/kbench.py, KB_LPW): 32 lanes
+// win when there are walkers enough for >= 4 waves per SIMD at two walkers per wave
+// (W >= 8192: -2 .. -8 % on configs 3 and 4), tie at W = 4096 with one planet and lose
+// at W = 4096 with three; 16 lanes lose everywhere.  NP > 3 spills at 32 lanes.
+inline int choose_lpw(int forced, int np, int n, long long W) {
+    (void)n;
+    if (forced) return forced;
+    return (np <= 3 && W >= 8192) ? 32 : 64;
+}
+
 template <int NP, bool MULTI, int SOLVER, bool TP>
 void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
                double *out, PostArgs post) {
+    if (SOLVER == 0) {
+        const int lpw = choose_lpw(d.lpw, NP, n, W);
+        if (lpw == 32) return launch_seg<NP, MULTI, TP, 32>(st, d, n, ni, th, W, stride, out, post);
+        if (lpw == 16) return launch_seg<NP, MULTI, TP, 16>(st, d, n, ni, th, W, stride, out, post);
+    }
     long long blocks;
     int wb;
     ll_grid<NP>(W, blocks, wb);
@@ -529,6 +681,11 @@ int rvk_set_option(rvk_handle *h, int32_t key, int32_t value) {
         if (value != 0 && value != 1) return fail(RVK_E_ARG, "solver must be 0 (fast) or 1 (reference Halley)");
         h->solver = value;
         h->launch = pick_ll(h->n_planets, h->n_inst > 1, value, RVK_TP_INLINE && h->par == RVK_PAR_PKEWTP);
+        return RVK_OK;
+    }
+    if (key == RVK_OPT_LPW) {
+        if (value != 0 && value != 16 && value != 32 && value != 64) return fail(RVK_E_ARG, "lpw must be 0, 16, 32 or 64");
+        h->lpw = value;
         return RVK_OK;
     }
     if (key == RVK_OPT_GRAPH) {

@@ -26,6 +26,7 @@ struct EpochData {
     const SC *tab;        // sin/cos table (rvk_math.h, kTabN entries)
     double t0;            // Trend reference time (model.py:486,491)
     int par;              // parameterisation code (RVK_PAR_*)
+    int lpw;              // lanes per walker: 0 = chosen per launch, else 64 / 32 / 16 (RVK_OPT_LPW)
 };
 
 // Optional log-posterior epilogue of the log-likelihood kernel (fit.py:3461-3495):
@@ -71,7 +72,8 @@ struct rvk_handle {
     rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
     int solver = 0;
     int graph = 0;                           // RVK_OPT_GRAPH
+    int lpw = 0;                             // RVK_OPT_LPW
 
-    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par}; }
+    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw}; }
     int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }
 };

@@ -500,6 +500,15 @@ __device__ __forceinline__ PlanetK uniform_pk(const PlanetK &q) {
     return pk;
 }
 
+// Every lane gets the sum of its 16-lane row (the DPP butterflies of wave_sum).
+__device__ __forceinline__ double row_sum(double v) {
+    v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v);   // row_half_mirror
+    v += dpp_d<0x140>(v);   // row_mirror
+    return v;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
     v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
     v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]

@@ -108,6 +108,10 @@ class RVEngine:
         """0 = production solver (default); 1 = ravest's Halley iteration restated."""
         _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_SOLVER, int(solver)))
 
+    def set_lanes_per_walker(self, lpw: int) -> None:
+        """0 = chosen per launch (default); 64, 32 or 16 lanes of a wave per walker (RVK_OPT_LPW)."""
+        _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_LPW, int(lpw)))
+
     def reserve(self, max_walkers: int) -> None:
         _lib.check(_lib.load().rvk_reserve(self._h, int(max_walkers)))
 

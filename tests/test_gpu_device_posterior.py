@@ -29,6 +29,16 @@ def test_device_posterior_vs_reference(name):
     assert_ll_close(got, case["log_prob"], what=f"device-{name}")
 
 
+@pytest.mark.parametrize("lpw", [16, 32])
+def test_device_posterior_segmented_layouts(lpw):
+    """The posterior epilogue in the 2- and 4-walkers-per-wave layouts (RVK_OPT_LPW)."""
+    for name in ("cfg2", "n7", "case3"):
+        case = load_case(name)
+        lpost = _posterior(case)
+        lpost.log_likelihood.engine.set_lanes_per_walker(lpw)
+        assert_ll_close(lpost.device_posterior()(case["theta_free"]), case["log_prob"], what=f"lpw{lpw}-{name}")
+
+
 @pytest.mark.parametrize("name", ["cfg3", "case3", "cfg4"])
 def test_device_posterior_tensor_path_equals_host_path(name):
     import torch

@@ -190,3 +190,28 @@ def test_hostile_inputs_do_not_fault():
     fin = np.isfinite(ref) & np.isfinite(ll) & (Mmax < 2.0 ** 50)
     assert fin.sum() >= 32
     assert np.all(np.abs(ll[fin] - ref[fin]) <= 1e-9 * np.maximum(1, np.abs(ref[fin])))
+
+
+@pytest.mark.parametrize("lpw", [16, 32, 64])
+@pytest.mark.parametrize("np_,ni,n,par,trend", [(1, 1, 256, "P K e w Tp", False), (1, 2, 100, "P K e w Tc", True),
+                                                (2, 1, 37, "P K secosw sesinw Tp", False),
+                                                (3, 3, 300, "P K e w Tp", True)])
+def test_lanes_per_walker_layouts_vs_oracle(lpw, np_, ni, n, par, trend):
+    """Every lanes-per-walker layout (RVK_OPT_LPW; 32/16 put 2/4 walkers in a wave) gives the
+    oracle's values: odd walker counts, a partial last wave, dead walkers, multi-instrument, trend."""
+    from oracle import oracle
+    from ravest_amd.engine import RVEngine
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(np_, n, ni, seed=200 + np_ + n, parameterisation=par, trend=trend)
+    th = make_walkers(ds, 4103, seed=7 + n)                # not a multiple of 4, 8 or 16; ~2% invalid
+    eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation, ds.t0)
+    eng.set_lanes_per_walker(lpw)
+    ll = eng.loglike(th)
+    ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation.code, ds.t0, th)
+    assert_ll_close(ll, ref, what=f"lpw{lpw}-np{np_}-n{n}")
+    assert (~np.isfinite(ll)).sum() > 0
+    big = make_walkers(ds, 70001, seed=3)                  # > 2048 blocks: multi-pass grid
+    ll2 = eng.loglike(big)
+    eng.set_lanes_per_walker(64)
+    assert np.array_equal(np.isfinite(ll2), np.isfinite(eng.loglike(big)))
+    assert_ll_close(ll2, eng.loglike(big), what=f"lpw{lpw}-vs-64-big")

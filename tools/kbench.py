@@ -48,6 +48,8 @@ def main():
         eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), len(ds.planet_letters),
                        ds.parameterisation, ds.t0, device=0)
         eng.reserve(len(ds.theta))
+        if os.environ.get("KB_LPW"):
+            eng.set_lanes_per_walker(int(os.environ["KB_LPW"]))
         th = torch.from_numpy(ds.theta).cuda(); out = torch.empty(len(ds.theta), dtype=torch.float64, device="cuda")
         row = {"case": name, "W": len(ds.theta), "N": len(ds.time), "NP": len(ds.planet_letters)}
         for solver in ((0, 1) if os.environ.get("KB_BOTH") else (0,)):
