@@ -15,12 +15,13 @@ LIB_PATH = os.path.join(_HERE, "lib", "librvk.so")
 # experiment hook: A/B builds of the same source (tools/variants.sh); never set in production
 LIB_PATH = os.environ.get("RAVEST_AMD_LIB", LIB_PATH)
 
-# every symbol declared in include/rvk.h and include/rvk_post.h
+# every symbol declared in include/rvk.h, include/rvk_post.h and include/rvk_gp.h
 EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rvk_reserve", "rvk_predict", "rvk_predict_device",
            "rvk_solve_kepler", "rvk_set_option", "rvk_stream", "rvk_sync", "rvk_device_count",
            "rvk_last_error", "rvk_version",
            "rvk_post_create", "rvk_post_destroy", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
-           "rvk_stretch_run"]
+           "rvk_stretch_run",
+           "rvk_gp_create", "rvk_gp_destroy", "rvk_gp_loglike", "rvk_gp_loglike_device"]
 
 OPT_SOLVER = 1
 OPT_GRAPH = 2
@@ -36,6 +37,8 @@ PRIOR_KIND = {"Uniform": 0, "EccentricityUniform": 1, "Normal": 2, "TruncatedNor
 
 
 POST_CONVERT = 1
+GP_QUASIPERIODIC = 0
+GP_NHYPER = 4
 
 
 def prior_src_default(planet: int, j: int) -> int:
@@ -90,7 +93,13 @@ def load() -> C.CDLL:
     L.rvk_logpost_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
     L.rvk_stretch_run.argtypes = [vp, vp, vp, C.c_int64, C.c_int32, C.c_double, C.c_uint64, C.c_uint64,
                                   vp, vp, vp, vp, vp, vp, vp, vp, vp]
-    for name in ("rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
+    L.rvk_gp_create.argtypes = [vp, C.c_int32]
+    L.rvk_gp_create.restype = vp
+    L.rvk_gp_destroy.argtypes = [vp]
+    L.rvk_gp_destroy.restype = None
+    L.rvk_gp_loglike.argtypes = [vp, dp, dp, C.c_int64, C.c_int64, C.c_int64, dp]
+    L.rvk_gp_loglike_device.argtypes = [vp, vp, vp, C.c_int64, C.c_int64, C.c_int64, vp, vp]
+    for name in ("rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
                  "rvk_set_option", "rvk_reserve", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
                  "rvk_stretch_run"):
         getattr(L, name).restype = C.c_int

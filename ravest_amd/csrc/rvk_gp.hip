@@ -1,0 +1,394 @@
+// rvk_gp.hip -- batched quasi-periodic GP log-likelihood (include/rvk_gp.h;
+// SURVEY.md §8(f) row 2, BASELINE config 5).
+//
+// One workgroup (4 waves) per walker, grid-stride over walkers.  Per walker:
+//   1. planet constants (lanes over planets) and the mean model in fp64 (the
+//      log-likelihood kernel's Kepler solver, threads over epochs) -> residuals
+//      r and the diagonal velerr^2 + jit^2 in LDS (fp32);
+//   2. the covariance's lower triangle, built straight into the walker's
+//      workspace as packed 32x32 tiles (fp32, tile (bi, bj), bi >= bj);
+//   3. right-looking blocked Cholesky with the right-hand side carried along
+//      (no triangular solve afterwards), per 32-column step kb:
+//        a. wave 0 factors the diagonal tile in LDS and solves its 32 rhs;
+//           log det and r^T C^-1 r accumulate in fp64;
+//        b. the panel below (rows of tiles (bi, kb)) is solved against L_kk^T,
+//           one thread per row, into LDS, and the rhs below is updated;
+//        c. the trailing lower triangle is updated C -= P P^T tile by tile
+//           with v_mfma_f32_32x32x2_f32 (16 per tile), operands from LDS.
+//   ll = -1/2 r^T C^-1 r - sum log L_ii - N/2 log(2 pi).
+// Padding rows/columns up to a multiple of 32 are identity rows with r = 0.
+#include <cmath>
+#include <vector>
+
+#include "../../include/rvk_gp.h"
+#include "rvk_internal.h"
+
+using namespace rvk;
+
+namespace {
+
+constexpr int TB = 32;              // tile edge
+constexpr int PS = TB + 1;          // LDS row stride of the panel / diagonal tile (bank spread)
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+__device__ __forceinline__ long long tile_index(int bi, int bj) { return (long long)bi * (bi + 1) / 2 + bj; }
+
+// MFMA 32x32 C/D map (cdna_hip_programming.md): register r of lane l holds
+// (row = (r & 3) + 8 (r >> 2) + 4 (l >> 5), col = l & 31).
+__device__ __forceinline__ int cd_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+struct GpLds {
+    // carved from dynamic shared memory
+    float *pan;      // [(npad - TB)][PS]  panel of the current step
+    float *dg;       // [TB][PS]           factored diagonal tile
+    float *r;        // [npad]             rhs (residuals), solved in place
+    float *dia;      // [npad]             velerr^2 + jit^2
+    SC *tab;         // [kTabN]
+    PlanetK *pk;     // [NP]
+    int *ok;         // [NP]
+};
+
+template <int NP, bool MULTI, bool TP>
+__global__ __launch_bounds__(kBlock) void gp_loglike_kernel(EpochData d, int n, int ni,
+                                                           const double *__restrict__ theta,
+                                                           const double *__restrict__ hyper, long long W,
+                                                           long long stride, long long hstride,
+                                                           float *__restrict__ work, long long work_stride,
+                                                           double *__restrict__ out) {
+    extern __shared__ double smem_d[];
+    const int nt = (n + TB - 1) / TB, npad = nt * TB;
+    GpLds L;
+    {
+        float *f = reinterpret_cast<float *>(smem_d);
+        L.pan = f;
+        f += (npad - TB) * PS;
+        L.dg = f;
+        f += TB * PS;
+        L.r = f;
+        f += npad;
+        L.dia = f;
+        f += npad;
+        L.tab = reinterpret_cast<SC *>(reinterpret_cast<uintptr_t>(f + 3) & ~uintptr_t(15));
+        L.pk = reinterpret_cast<PlanetK *>(L.tab + kTabN);
+        L.ok = reinterpret_cast<int *>(L.pk + NP);
+    }
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < kTabN; i += kBlock) L.tab[i] = d.tab[i];
+    float *A = work + (long long)blockIdx.x * work_stride;
+
+    for (long long w = blockIdx.x; w < W; w += gridDim.x) {
+        const double *row = theta + w * stride;
+        const double *hp = hyper + w * hstride;
+        // ---- 1. planets, mean model, residuals -------------------------------------------
+        if (tid < NP) {
+            PlanetK pk;
+            const bool ok = TP ? planet_consts_t<0, true>(row + 5 * tid, pk, 0, L.tab)
+                               : planet_consts(d.par, row + 5 * tid, pk);
+            L.pk[tid] = pk;
+            L.ok[tid] = ok;
+        }
+        __syncthreads();   // (the table fill of the first trip lands here too)
+        bool alive = true;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) alive &= L.ok[p] != 0;
+        if (!alive) {                                   // fit.py:8083-8085: mean model failed
+            if (tid == 0) out[w] = -INFINITY;
+            __syncthreads();
+            continue;
+        }
+        const double *g = row + 5 * NP, *jit = g + ni;
+        const double gd = jit[ni], gdd = jit[ni + 1];
+        for (int i = tid; i < npad; i += kBlock) {
+            float ri = 0.0f, di = 1.0f;
+            if (i < n) {
+                const double t = d.t[i];
+                const int ii = MULTI ? d.inst[i] : 0;
+                double rv = 0.0;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) rv = planet_rv<0>(L.pk[p], t, L.tab, rv);
+                const double dt = t - d.t0;
+                rv += __builtin_fma(gd, dt, gdd * (dt * dt));      // Trend (fit.py:8031-8035)
+                rv += g[ii];                                       // gamma (fit.py:8041-8045)
+                ri = (float)(d.vel[i] - rv);
+                di = (float)(d.s2[i] + jit[ii] * jit[ii]);         // fit.py:8096-8098
+            }
+            L.r[i] = ri;
+            L.dia[i] = di;
+        }
+        __syncthreads();
+        // ---- 2. covariance tiles (lower triangle) ----------------------------------------
+        const double amp = hp[0], lam_e = hp[1], lam_p = hp[2], per = hp[3];
+        const float amp2 = (float)(amp * amp);
+        const float gam = (float)(1.0 / (2.0 * lam_p * lam_p));   // gp.py:150
+        const double inv_per = 1.0 / per, inv_le = 1.0 / lam_e;
+        const int ntiles = nt * (nt + 1) / 2;
+        for (int t = wv; t < ntiles; t += kWavesPerBlock) {
+            int bi = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+            while (bi * (bi + 1) / 2 > t) --bi;
+            while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+            const int bj = t - bi * (bi + 1) / 2;
+            float *T = A + (long long)t * (TB * TB);
+            const int col = lane & 31, j = bj * TB + col;
+            const double tj = j < n ? d.t[j] : 0.0;
+#pragma unroll 4
+            for (int r = 0; r < 16; ++r) {
+                const int rr = cd_row(r, lane), i = bi * TB + rr;
+                float v;
+                if (i >= n || j >= n) {
+                    v = (i == j) ? 1.0f : 0.0f;
+                } else {
+                    const double tau = d.t[i] - tj;
+                    // sin^2(pi tau / P) from the phase reduced in fp64, then fp32
+                    const double ph = tau * inv_per;
+                    const float fr = (float)(ph - __builtin_rint(ph));
+                    const float s = __builtin_amdgcn_sinf(0.5f * fr);     // v_sin_f32 takes revolutions
+                    const float x = (float)(tau * inv_le);
+                    v = amp2 * __expf(-(gam * (s * s) + 0.5f * (x * x)));
+                    if (i == j) v += L.dia[i];
+                }
+                T[rr * TB + col] = v;
+            }
+        }
+        __syncthreads();
+        // ---- 3. blocked Cholesky with the rhs carried along ------------------------------
+        double logdet = 0.0, quad = 0.0;    // meaningful in thread 0
+        for (int kb = 0; kb < nt; ++kb) {
+            // a. diagonal tile: factor in LDS, solve its rhs (wave 0)
+            if (wv == 0) {
+                const float *T = A + tile_index(kb, kb) * (TB * TB);
+                for (int e = lane; e < TB * TB; e += 64) L.dg[(e / TB) * PS + (e % TB)] = T[e];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int c = 0; c < TB; ++c) {
+                    const float dc = __builtin_sqrtf(L.dg[c * PS + c]);
+                    const float inv = 1.0f / dc;
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane > c && lane < TB) L.dg[lane * PS + c] *= inv;
+                    if (lane == c) L.dg[c * PS + c] = dc;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // rank-1 update of the lower-right part: lane = row i, half-waves split the columns
+                    const int i = lane & 31;
+                    if (i > c) {
+                        const float lic = L.dg[i * PS + c];
+                        for (int jj = c + 1 + (lane >> 5); jj <= i; jj += 2)
+                            L.dg[i * PS + jj] -= lic * L.dg[jj * PS + c];
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+                // forward substitution of the block's rhs: y_c = (r_c - sum_{c'<c} L_cc' y_c') / L_cc
+                float* rb = L.r + kb * TB;
+                for (int c = 0; c < TB; ++c) {
+                    const float yc = rb[c] / L.dg[c * PS + c];
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane > c && lane < TB) rb[lane] -= L.dg[lane * PS + c] * yc;
+                    if (lane == c) rb[c] = yc;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (lane == 0 && kb * TB + c < n) {
+                        logdet += log((double)L.dg[c * PS + c]);
+                        quad += (double)yc * (double)yc;
+                    }
+                }
+            }
+            __syncthreads();
+            const int m = nt - kb - 1;               // tiles below the diagonal
+            if (m == 0) break;
+            // b. panel rows: x = a L_kk^-T (one thread per row), rhs below -= x . y
+            for (int ri = tid; ri < m * TB; ri += kBlock) {
+                const int bi = kb + 1 + ri / TB, rr = ri % TB;
+                const float *src = A + tile_index(bi, kb) * (TB * TB) + rr * TB;
+                float x[TB];
+#pragma unroll
+                for (int c = 0; c < TB; c += 4) {
+                    const float4 v = *reinterpret_cast<const float4 *>(src + c);
+                    x[c] = v.x; x[c + 1] = v.y; x[c + 2] = v.z; x[c + 3] = v.w;
+                }
+                float acc = 0.0f;
+#pragma unroll
+                for (int c = 0; c < TB; ++c) {
+                    float s = x[c];
+#pragma unroll
+                    for (int cc = 0; cc < c; ++cc) s -= x[cc] * L.dg[c * PS + cc];
+                    x[c] = s / L.dg[c * PS + c];
+                    acc += x[c] * L.r[kb * TB + c];
+                    L.pan[ri * PS + c] = x[c];
+                }
+                L.r[(kb + 1) * TB + ri] -= acc;
+            }
+            __syncthreads();
+            // c. trailing update C -= P P^T on the lower triangle of tiles
+            const int cnt = m * (m + 1) / 2;
+            for (int t = wv; t < cnt; t += kWavesPerBlock) {
+                int a = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+                while (a * (a + 1) / 2 > t) --a;
+                while ((a + 1) * (a + 2) / 2 <= t) ++a;
+                const int b = t - a * (a + 1) / 2;                 // 0 <= b <= a < m
+                float *C = A + tile_index(kb + 1 + a, kb + 1 + b) * (TB * TB);
+                const int col = lane & 31;
+                f32x16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = C[cd_row(r, lane) * TB + col];
+                const float *pa = L.pan + (a * TB + (lane & 31)) * PS + (lane >> 5);
+                const float *pb = L.pan + (b * TB + (lane & 31)) * PS + (lane >> 5);
+#pragma unroll
+                for (int s = 0; s < TB / 2; ++s)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(-pa[2 * s], pb[2 * s], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) C[cd_row(r, lane) * TB + col] = acc[r];
+            }
+            __syncthreads();
+        }
+        if (tid == 0) out[w] = -0.5 * quad - logdet - 0.5 * (double)n * kLog2Pi;
+        __syncthreads();
+    }
+}
+
+size_t gp_lds_bytes(int n, int np) {
+    const int npad = ((n + TB - 1) / TB) * TB;
+    size_t b = sizeof(float) * ((size_t)(npad - TB) * PS + TB * PS + 2 * (size_t)npad) + 16;
+    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
+    return b;
+}
+
+typedef void (*gp_launch_t)(hipStream_t, unsigned, size_t, EpochData, int, int, const double *, const double *,
+                            long long, long long, long long, float *, long long, double *);
+
+template <int NP, bool MULTI, bool TP>
+void launch_gp(hipStream_t st, unsigned grid, size_t lds, EpochData d, int n, int ni, const double *th,
+               const double *hy, long long W, long long stride, long long hs, float *work, long long wstride,
+               double *out) {
+    static size_t allowed = 0;   // dynamic LDS beyond the default needs the attribute
+    if (lds > allowed) {
+        (void)hipFuncSetAttribute((const void *)gp_loglike_kernel<NP, MULTI, TP>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        allowed = lds;
+    }
+    hipLaunchKernelGGL((gp_loglike_kernel<NP, MULTI, TP>), dim3(grid), dim3(kBlock), lds, st, d, n, ni, th, hy, W,
+                       stride, hs, work, wstride, out);
+}
+
+template <bool MULTI, bool TP>
+gp_launch_t pick_gp_s(int np) {
+    switch (np) {
+        case 1: return launch_gp<1, MULTI, TP>;
+        case 2: return launch_gp<2, MULTI, TP>;
+        case 3: return launch_gp<3, MULTI, TP>;
+        case 4: return launch_gp<4, MULTI, TP>;
+        case 5: return launch_gp<5, MULTI, TP>;
+        case 6: return launch_gp<6, MULTI, TP>;
+        case 7: return launch_gp<7, MULTI, TP>;
+        case 8: return launch_gp<8, MULTI, TP>;
+        default: return nullptr;
+    }
+}
+
+gp_launch_t pick_gp(int np, bool multi, bool tp) {
+    if (multi) return tp ? pick_gp_s<true, true>(np) : pick_gp_s<true, false>(np);
+    return tp ? pick_gp_s<false, true>(np) : pick_gp_s<false, false>(np);
+}
+
+}  // namespace
+
+struct rvk_gp {
+    rvk_handle *h = nullptr;
+    gp_launch_t launch = nullptr;
+    unsigned grid = 0;           // concurrent walkers (one workgroup each)
+    size_t lds = 0;
+    long long wstride = 0;       // floats per workgroup workspace
+    float *d_work = nullptr;
+};
+
+static void free_gp(rvk_gp *g) {
+    if (!g) return;
+    if (g->h) (void)hipSetDevice(g->h->device);
+    (void)hipFree(g->d_work);
+    delete g;
+}
+
+static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
+    if (!h) return fail(RVK_E_ARG, "NULL handle");
+    if (kernel != RVK_GP_QUASIPERIODIC) return fail(RVK_E_ARG, "unknown GP kernel type");
+    if (h->n < 1 || h->n > RVK_GP_MAX_EPOCHS) return fail(RVK_E_ARG, "GP needs 1 <= n_epochs <= 1024");
+    g->h = h;
+    g->launch = pick_gp(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP);
+    g->lds = gp_lds_bytes(h->n, h->n_planets);
+    HIPCHK(hipSetDevice(h->device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, h->device));
+    // workgroups that fit at once (LDS-limited), each with its own workspace
+    const size_t per_cu = (size_t)160 * 1024 / g->lds;
+    g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu)));
+    const int nt = (h->n + TB - 1) / TB;
+    g->wstride = (long long)nt * (nt + 1) / 2 * TB * TB;
+    HIPCHK(hipMalloc(&g->d_work, sizeof(float) * (size_t)g->wstride * g->grid));
+    return RVK_OK;
+}
+
+extern "C" {
+
+rvk_gp *rvk_gp_create(rvk_handle *h, int32_t kernel_type) {
+    rvk_gp *g = new (std::nothrow) rvk_gp();
+    if (!g) {
+        fail(RVK_E_NOMEM, "out of host memory");
+        return nullptr;
+    }
+    if (create_gp(g, h, kernel_type)) {
+        free_gp(g);
+        return nullptr;
+    }
+    return g;
+}
+
+void rvk_gp_destroy(rvk_gp *g) { free_gp(g); }
+
+int rvk_gp_loglike_device(rvk_gp *g, const double *d_theta, const double *d_hyper, int64_t W, int64_t stride,
+                          int64_t hstride, double *d_out, void *stream) {
+    if (!g) return fail(RVK_E_ARG, "NULL GP handle");
+    rvk_handle *h = g->h;
+    if (W < 0 || stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad walker block shape");
+    if (W == 0) return RVK_OK;
+    if (!d_theta || !d_hyper || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
+    HIPCHK(hipSetDevice(h->device));
+    const unsigned grid = (unsigned)((long long)g->grid < W ? g->grid : W);
+    g->launch((hipStream_t)stream, grid, g->lds, h->epochs(), h->n, h->n_inst, d_theta, d_hyper, W, stride, hstride,
+              g->d_work, g->wstride, d_out);
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t W, int64_t stride, int64_t hstride,
+                   double *out) {
+    if (!g) return fail(RVK_E_ARG, "NULL GP handle");
+    if (W == 0) return RVK_OK;
+    if (!theta || !hyper || !out || W < 0) return fail(RVK_E_ARG, "bad host buffers");
+    rvk_handle *h = g->h;
+    HIPCHK(hipSetDevice(h->device));
+    double *dt = nullptr, *dh = nullptr, *dout = nullptr;
+    const size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bh = sizeof(double) * (size_t)W * (size_t)hstride;
+    int rc = RVK_OK;
+    if (hipMalloc(&dt, bt) != hipSuccess || hipMalloc(&dh, bh) != hipSuccess ||
+        hipMalloc(&dout, sizeof(double) * (size_t)W) != hipSuccess)
+        rc = fail(RVK_E_HIP, "hipMalloc failed");
+    if (rc == RVK_OK && (hipMemcpyAsync(dt, theta, bt, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+                         hipMemcpyAsync(dh, hyper, bh, hipMemcpyHostToDevice, h->stream) != hipSuccess))
+        rc = fail(RVK_E_HIP, "hipMemcpyAsync H2D failed");
+    if (rc == RVK_OK) rc = rvk_gp_loglike_device(g, dt, dh, W, stride, hstride, dout, h->stream);
+    if (rc == RVK_OK &&
+        hipMemcpyAsync(out, dout, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+        rc = fail(RVK_E_HIP, "hipMemcpyAsync D2H failed");
+    if (hipStreamSynchronize(h->stream) != hipSuccess && rc == RVK_OK) rc = fail(RVK_E_HIP, "stream sync failed");
+    (void)hipFree(dt);
+    (void)hipFree(dh);
+    (void)hipFree(dout);
+    return rc;
+}
+
+}  // extern "C"

@@ -24,6 +24,7 @@ CONFIGS = {
     2: dict(seed=2, n_planets=1, n_epochs=256, n_walkers=4096, n_inst=1),
     3: dict(seed=3, n_planets=3, n_epochs=1024, n_walkers=16384, n_inst=2),
     4: dict(seed=4, n_planets=2, n_epochs=512, n_walkers=65536, n_inst=1),
+    5: dict(seed=5, n_planets=1, n_epochs=512, n_walkers=4096, n_inst=1),   # + quasi-periodic GP
 }
 
 LETTERS = "bcdefghi"
@@ -180,3 +181,26 @@ def make_posterior(config: int = 2, n_walkers: int | None = None, device: int = 
     rng = np.random.default_rng(seed)
     x0 = np.array([ds.truth[n] for n in free])[None, :] * (1 + 1e-4 * rng.standard_normal((W, len(free))))
     return lpost, x0
+
+
+def make_gp_config(n_walkers: int | None = None, n_epochs: int = 512, seed: int = 5, n_planets: int = 1,
+                   n_inst: int = 1):
+    """BASELINE config 5: one planet + quasi-periodic GP residuals.  Returns (dataset,
+    theta [W, P_full], hyper [W, 4] (gp_amp, gp_lambda_e, gp_lambda_p, gp_period)).
+    The data are a Keplerian plus one draw of the GP (fp64 Cholesky of the truth's
+    covariance) plus white noise; walkers are a 5 % ball around the truth (2 % with a
+    broken planet, as in make_walkers)."""
+    rng = np.random.default_rng(seed + 77)
+    ds = make_dataset(n_planets, n_epochs, n_inst, seed=seed)
+    hyper0 = np.array([rng.uniform(3, 6), rng.uniform(40, 90), rng.uniform(0.4, 0.8), rng.uniform(15, 30)])
+    amp, lam_e, lam_p, per = hyper0
+    tau = np.subtract.outer(ds.time, ds.time)
+    K = amp ** 2 * np.exp(-np.sin(np.pi * np.abs(tau) / per) ** 2 / (2 * lam_p ** 2)) * np.exp(-0.5 * (tau / lam_e) ** 2)
+    Lc = np.linalg.cholesky(K + 1e-8 * amp ** 2 * np.eye(n_epochs))
+    ds.vel = ds.vel + Lc @ rng.standard_normal(n_epochs)
+    W = n_walkers or CONFIGS[5]["n_walkers"]
+    theta = make_walkers(ds, W, seed=seed)
+    hyper = hyper0[None, :] * (1 + 0.05 * rng.standard_normal((W, 4)))
+    hyper = np.abs(hyper)
+    ds.truth.update(dict(zip(["gp_amp", "gp_lambda_e", "gp_lambda_p", "gp_period"], hyper0)))
+    return ds, theta, hyper

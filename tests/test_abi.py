@@ -11,7 +11,7 @@ from tests.conftest import ROOT
 
 def _declared():
     names = set()
-    for hdr in ("rvk.h", "rvk_post.h"):
+    for hdr in ("rvk.h", "rvk_post.h", "rvk_gp.h"):
         src = open(os.path.join(ROOT, "include", hdr)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         src = re.sub(r"#define.*", "", src)
@@ -60,6 +60,8 @@ def test_bad_arguments_fail_loudly():
     assert L.rvk_logpost_device(None, None, 1, 1, None, None) == -1
     assert L.rvk_stretch_run(None, None, None, 8, 1, 2.0, 0, 0, None, None, None, None, None, None, None, None,
                              None) == -1
+    assert not L.rvk_gp_create(None, 0) and "handle" in _lib.last_error()
+    assert L.rvk_gp_loglike_device(None, None, None, 1, 9, 4, None, None) == -1
 
 
 def test_engine_raises_without_library(monkeypatch, tmp_path):

@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 rm -rf build/variants && mkdir -p build/variants
 build() { name=$1; shift; /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
-  -o build/variants/librvk_$name.so ravest_amd/csrc/rvk.hip ravest_amd/csrc/rvk_post.hip 2>/dev/null & }
+  -o build/variants/librvk_$name.so ravest_amd/csrc/rvk.hip ravest_amd/csrc/rvk_post.hip ravest_amd/csrc/rvk_gp.hip 2>/dev/null & }
 build base
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
