@@ -27,10 +27,20 @@ using namespace rvk;
 
 namespace {
 
+#ifndef RVK_GP_ABLATE
+#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 no trailing update, 2 no panel, 4 no build
+#endif
+#ifndef RVK_GP_WGPCU
+#define RVK_GP_WGPCU 2    // concurrent workgroups per CU (each its own workspace), LDS permitting
+#endif
 constexpr int TB = 32;              // tile edge
 constexpr int PS = TB + 1;          // LDS row stride of the panel / diagonal tile (bank spread)
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+__device__ __forceinline__ float rlf(float v, int lane) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
 
 __device__ __forceinline__ long long tile_index(int bi, int bj) { return (long long)bi * (bi + 1) / 2 + bj; }
 
@@ -41,7 +51,8 @@ __device__ __forceinline__ int cd_row(int r, int lane) { return (r & 3) + 8 * (r
 struct GpLds {
     // carved from dynamic shared memory
     float *pan;      // [(npad - TB)][PS]  panel of the current step
-    float *dg;       // [TB][PS]           factored diagonal tile
+    float *dg;       // [TB][PS]           factored diagonal tile (1 / L_ii on the diagonal)
+    float *li;       // [TB][PS]           its inverse
     float *r;        // [npad]             rhs (residuals), solved in place
     float *dia;      // [npad]             velerr^2 + jit^2
     SC *tab;         // [kTabN]
@@ -50,7 +61,7 @@ struct GpLds {
 };
 
 template <int NP, bool MULTI, bool TP>
-__global__ __launch_bounds__(kBlock) void gp_loglike_kernel(EpochData d, int n, int ni,
+__global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int n, int ni,
                                                            const double *__restrict__ theta,
                                                            const double *__restrict__ hyper, long long W,
                                                            long long stride, long long hstride,
@@ -64,6 +75,8 @@ __global__ __launch_bounds__(kBlock) void gp_loglike_kernel(EpochData d, int n, 
         L.pan = f;
         f += (npad - TB) * PS;
         L.dg = f;
+        f += TB * PS;
+        L.li = f;
         f += TB * PS;
         L.r = f;
         f += npad;
@@ -123,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void gp_loglike_kernel(EpochData d, int n, 
         const float amp2 = (float)(amp * amp);
         const float gam = (float)(1.0 / (2.0 * lam_p * lam_p));   // gp.py:150
         const double inv_per = 1.0 / per, inv_le = 1.0 / lam_e;
-        const int ntiles = nt * (nt + 1) / 2;
+        const int ntiles = (RVK_GP_ABLATE & 4) ? 0 : nt * (nt + 1) / 2;
         for (int t = wv; t < ntiles; t += kWavesPerBlock) {
             int bi = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
             while (bi * (bi + 1) / 2 > t) --bi;
@@ -155,94 +168,128 @@ __global__ __launch_bounds__(kBlock) void gp_loglike_kernel(EpochData d, int n, 
         // ---- 3. blocked Cholesky with the rhs carried along ------------------------------
         double logdet = 0.0, quad = 0.0;    // meaningful in thread 0
         for (int kb = 0; kb < nt; ++kb) {
-            // a. diagonal tile: factor in LDS, solve its rhs (wave 0)
+            // lane-derived addresses are recomputed per step, not hoisted and held for the kernel
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            // a. diagonal tile (wave 0), in registers: lane i holds row i; the pivots and the
+            //    column entries other lanes need are broadcast with v_readlane (no LDS, no
+            //    barriers).  Then the block's rhs by forward substitution, and L_kk (+ the
+            //    reciprocals of its diagonal) to LDS for the panel.
             if (wv == 0) {
-                const float *T = A + tile_index(kb, kb) * (TB * TB);
-                for (int e = lane; e < TB * TB; e += 64) L.dg[(e / TB) * PS + (e % TB)] = T[e];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int c = 0; c < TB; ++c) {
-                    const float dc = __builtin_sqrtf(L.dg[c * PS + c]);
-                    const float inv = 1.0f / dc;
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane > c && lane < TB) L.dg[lane * PS + c] *= inv;
-                    if (lane == c) L.dg[c * PS + c] = dc;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // rank-1 update of the lower-right part: lane = row i, half-waves split the columns
-                    const int i = lane & 31;
-                    if (i > c) {
-                        const float lic = L.dg[i * PS + c];
-                        for (int jj = c + 1 + (lane >> 5); jj <= i; jj += 2)
-                            L.dg[i * PS + jj] -= lic * L.dg[jj * PS + c];
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int i = ln & 31;
+                const float *src = A + tile_index(kb, kb) * (TB * TB) + i * TB;
+                float a[TB];
+#pragma unroll
+                for (int c = 0; c < TB; c += 4) {
+                    const float4 v = *reinterpret_cast<const float4 *>(src + c);
+                    a[c] = v.x; a[c + 1] = v.y; a[c + 2] = v.z; a[c + 3] = v.w;
                 }
-                // forward substitution of the block's rhs: y_c = (r_c - sum_{c'<c} L_cc' y_c') / L_cc
-                float* rb = L.r + kb * TB;
-                for (int c = 0; c < TB; ++c) {
-                    const float yc = rb[c] / L.dg[c * PS + c];
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane > c && lane < TB) rb[lane] -= L.dg[lane * PS + c] * yc;
-                    if (lane == c) rb[c] = yc;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    if (lane == 0 && kb * TB + c < n) {
-                        logdet += log((double)L.dg[c * PS + c]);
-                        quad += (double)yc * (double)yc;
+                const float rb = L.r[kb * TB + i];
+                // Left-looking, one column per step r: row r of L (lane r's finished entries
+                // L[r][k], k < r) is broadcast with v_readlane and shared by the column update
+                // a_i[r] -= sum_k a_i[k] L[r][k], the rhs y_r and the inverse's row
+                // X[r][j] = (delta_rj - sum_k L[r][k] X[k][j]) / L[r][r] (lane j = column j).
+                float xinv[TB], y[TB];
+                double dprod = 1.0;                   // log det via products of 8 pivots
+                float yown = 0.0f;                    // y[i]
+#pragma unroll
+                for (int r = 0; r < TB; ++r) {
+                    float col = a[r], xs = (r == i) ? 1.0f : 0.0f, ys = rlf(rb, r);
+#pragma unroll
+                    for (int k = 0; k < r; ++k) {
+                        const float lrk = rlf(a[k], r);
+                        col = __builtin_fmaf(-a[k], lrk, col);
+                        xs = __builtin_fmaf(-lrk, xinv[k], xs);
+                        ys = __builtin_fmaf(-lrk, y[k], ys);
                     }
+                    const float dc = __builtin_sqrtf(rlf(col, r));    // not positive definite -> NaN
+                    const float inv = 1.0f / dc;
+                    a[r] = (i == r) ? dc : col * inv;                 // rows i < r: upper part, unused
+                    xinv[r] = xs * inv;
+                    y[r] = ys * inv;
+                    yown = (i == r) ? y[r] : yown;
+                    asm volatile("" : "+v"(xinv[r]), "+v"(y[r]), "+v"(a[r]), "+v"(yown));   // finish step r here
+                    const bool live = kb * TB + r < n;
+                    dprod *= live ? (double)dc : 1.0;
+                    quad += live ? (double)y[r] * (double)y[r] : 0.0;
+                    if ((r & 7) == 7) { logdet += log(dprod); dprod = 1.0; }
+                }
+                if (ln < TB) {
+#pragma unroll
+                    for (int c = 0; c < TB; ++c) L.dg[i * PS + c] = (c == i) ? 1.0f / a[c] : a[c];
+                    L.r[kb * TB + i] = yown;
+                }
+                if (ln < TB) {
+#pragma unroll
+                    for (int r = 0; r < TB; ++r) L.li[r * PS + i] = xinv[r];   // Linv, row-major
                 }
             }
             __syncthreads();
             const int m = nt - kb - 1;               // tiles below the diagonal
             if (m == 0) break;
-            // b. panel rows: x = a L_kk^-T (one thread per row), rhs below -= x . y
-            for (int ri = tid; ri < m * TB; ri += kBlock) {
-                const int bi = kb + 1 + ri / TB, rr = ri % TB;
-                const float *src = A + tile_index(bi, kb) * (TB * TB) + rr * TB;
-                float x[TB];
+            // b. panel tiles P = A_(bi,kb) L_kk^-T with MFMA (16 per tile), waves over tiles, into
+            //    LDS; then the rhs below: r_i -= P_i . y (threads over rows)
+            for (int a = wv; a < ((RVK_GP_ABLATE & 2) ? 0 : m); a += kWavesPerBlock) {
+                // A operand: lane l holds A[l & 31][2 ks + (l >> 5)]
+                const float *src = A + tile_index(kb + 1 + a, kb) * (TB * TB) + (ln & 31) * TB + (ln >> 5);
+                float av[TB / 2];
 #pragma unroll
-                for (int c = 0; c < TB; c += 4) {
-                    const float4 v = *reinterpret_cast<const float4 *>(src + c);
-                    x[c] = v.x; x[c + 1] = v.y; x[c + 2] = v.z; x[c + 3] = v.w;
-                }
+                for (int ks = 0; ks < TB / 2; ++ks) av[ks] = src[2 * ks];
+                f32x16 acc = {};
+                const float *lb = L.li + (ln & 31) * PS + (ln >> 5);   // B[k][j] = Linv[j][k]
+#pragma unroll
+                for (int ks = 0; ks < TB / 2; ++ks)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ks], lb[2 * ks], acc, 0, 0, 0);
+                const int col = ln & 31;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) L.pan[(a * TB + cd_row(r, ln)) * PS + col] = acc[r];
+            }
+            __syncthreads();
+            for (int ri = tid; ri < m * TB; ri += kBlock) {
                 float acc = 0.0f;
 #pragma unroll
-                for (int c = 0; c < TB; ++c) {
-                    float s = x[c];
-#pragma unroll
-                    for (int cc = 0; cc < c; ++cc) s -= x[cc] * L.dg[c * PS + cc];
-                    x[c] = s / L.dg[c * PS + c];
-                    acc += x[c] * L.r[kb * TB + c];
-                    L.pan[ri * PS + c] = x[c];
-                }
+                for (int c = 0; c < TB; ++c) acc = __builtin_fmaf(L.pan[ri * PS + c], L.r[kb * TB + c], acc);
                 L.r[(kb + 1) * TB + ri] -= acc;
             }
             __syncthreads();
             // c. trailing update C -= P P^T on the lower triangle of tiles
-            const int cnt = m * (m + 1) / 2;
-            for (int t = wv; t < cnt; t += kWavesPerBlock) {
-                int a = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+            const int cnt = (RVK_GP_ABLATE & 1) ? 0 : m * (m + 1) / 2;
+            const int col = ln & 31;
+            auto tile_of = [&](int t, int &a, int &b) {
+                a = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
                 while (a * (a + 1) / 2 > t) --a;
                 while ((a + 1) * (a + 2) / 2 <= t) ++a;
-                const int b = t - a * (a + 1) / 2;                 // 0 <= b <= a < m
-                float *C = A + tile_index(kb + 1 + a, kb + 1 + b) * (TB * TB);
-                const int col = lane & 31;
-                f32x16 acc;
+                b = t - a * (a + 1) / 2;                           // 0 <= b <= a < m
+            };
+            f32x16 cur;
+            int ta, tb;
+            if (wv < cnt) {
+                tile_of(wv, ta, tb);
+                const float *C = A + tile_index(kb + 1 + ta, kb + 1 + tb) * (TB * TB);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[r] = C[cd_row(r, lane) * TB + col];
-                const float *pa = L.pan + (a * TB + (lane & 31)) * PS + (lane >> 5);
-                const float *pb = L.pan + (b * TB + (lane & 31)) * PS + (lane >> 5);
+                for (int r = 0; r < 16; ++r) cur[r] = C[cd_row(r, ln) * TB + col];
+            }
+            for (int t = wv; t < cnt; t += kWavesPerBlock) {
+                // the next tile's loads are in flight during this tile's MFMAs
+                f32x16 nxt;
+                int na = 0, nb2 = 0;
+                if (t + kWavesPerBlock < cnt) {
+                    tile_of(t + kWavesPerBlock, na, nb2);
+                    const float *Cn = A + tile_index(kb + 1 + na, kb + 1 + nb2) * (TB * TB);
 #pragma unroll
-                for (int s = 0; s < TB / 2; ++s)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(-pa[2 * s], pb[2 * s], acc, 0, 0, 0);
+                    for (int r = 0; r < 16; ++r) nxt[r] = Cn[cd_row(r, ln) * TB + col];
+                }
+                const float *pa = L.pan + (ta * TB + (ln & 31)) * PS + (ln >> 5);
+                const float *pb = L.pan + (tb * TB + (ln & 31)) * PS + (ln >> 5);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) C[cd_row(r, lane) * TB + col] = acc[r];
+                for (int ks = 0; ks < TB / 2; ++ks)
+                    cur = __builtin_amdgcn_mfma_f32_32x32x2f32(-pa[2 * ks], pb[2 * ks], cur, 0, 0, 0);
+                float *C = A + tile_index(kb + 1 + ta, kb + 1 + tb) * (TB * TB);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) C[cd_row(r, ln) * TB + col] = cur[r];
+                cur = nxt;
+                ta = na;
+                tb = nb2;
             }
             __syncthreads();
         }
@@ -253,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void gp_loglike_kernel(EpochData d, int n, 
 
 size_t gp_lds_bytes(int n, int np) {
     const int npad = ((n + TB - 1) / TB) * TB;
-    size_t b = sizeof(float) * ((size_t)(npad - TB) * PS + TB * PS + 2 * (size_t)npad) + 16;
+    size_t b = sizeof(float) * ((size_t)(npad - TB) * PS + 2 * TB * PS + 2 * (size_t)npad) + 16;
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
     return b;
 }
@@ -325,7 +372,7 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     HIPCHK(hipGetDeviceProperties(&prop, h->device));
     // workgroups that fit at once (LDS-limited), each with its own workspace
     const size_t per_cu = (size_t)160 * 1024 / g->lds;
-    g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu)));
+    g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > RVK_GP_WGPCU ? RVK_GP_WGPCU : per_cu)));
     const int nt = (h->n + TB - 1) / TB;
     g->wstride = (long long)nt * (nt + 1) / 2 * TB * TB;
     HIPCHK(hipMalloc(&g->d_work, sizeof(float) * (size_t)g->wstride * g->grid));
