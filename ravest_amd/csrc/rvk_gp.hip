@@ -5,16 +5,16 @@
 //   1. planet constants (lanes over planets) and the mean model in fp64 (the
 //      log-likelihood kernel's Kepler solver, threads over epochs) -> residuals
 //      r and the diagonal velerr^2 + jit^2 in LDS (fp32);
-//   2. the covariance's lower triangle, built straight into the walker's
-//      workspace as packed 32x32 tiles (fp32, tile (bi, bj), bi >= bj);
-//   3. right-looking blocked Cholesky with the right-hand side carried along
-//      (no triangular solve afterwards), per 32-column step kb:
-//        a. wave 0 factors the diagonal tile in LDS and solves its 32 rhs;
-//           log det and r^T C^-1 r accumulate in fp64;
-//        b. the panel below (rows of tiles (bi, kb)) is solved against L_kk^T,
-//           one thread per row, into LDS, and the rhs below is updated;
-//        c. the trailing lower triangle is updated C -= P P^T tile by tile
-//           with v_mfma_f32_32x32x2_f32 (16 per tile), operands from LDS.
+//   2. left-looking blocked Cholesky over 32-column steps kb with the right-hand
+//      side carried along (no triangular solve afterwards).  The covariance is
+//      never stored: each tile (bi, kb) is generated in registers when its step
+//      comes, and only the finished L tiles below the diagonal go to the
+//      walker's workspace (packed 32x32 tiles, fp32), read back by later steps:
+//        a. all waves: pre = C_(bi,kb) - sum_j L_(bi,j) L_(kb,j)^T with
+//           v_mfma_f32_32x32x2_f32 (wave 0 the diagonal tile and its rhs);
+//        b. wave 0 factors the diagonal tile in registers (v_readlane broadcasts),
+//           its rhs and inverse, log det and r^T C^-1 r in fp64;
+//        c. all waves: L_(bi,kb) = pre L_kk^-T with MFMA, stored.
 //   ll = -1/2 r^T C^-1 r - sum log L_ii - N/2 log(2 pi).
 // Padding rows/columns up to a multiple of 32 are identity rows with r = 0.
 #include <cmath>
@@ -28,7 +28,7 @@ using namespace rvk;
 namespace {
 
 #ifndef RVK_GP_ABLATE
-#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 no trailing update, 2 no panel, 4 no build
+#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 no off-diagonal accumulation, 2 no solve
 #endif
 #ifndef RVK_GP_WGPCU
 #define RVK_GP_WGPCU 2    // concurrent workgroups per CU (each its own workspace), LDS permitting
@@ -50,9 +50,8 @@ __device__ __forceinline__ int cd_row(int r, int lane) { return (r & 3) + 8 * (r
 
 struct GpLds {
     // carved from dynamic shared memory
-    float *pan;      // [(npad - TB)][PS]  panel of the current step
-    float *dg;       // [TB][PS]           factored diagonal tile (1 / L_ii on the diagonal)
-    float *li;       // [TB][PS]           its inverse
+    float *pan;      // [(npad - TB)][TB]  the step's tiles below the diagonal, before the solve
+    float *li;       // [TB][PS]           inverse of the step's diagonal tile
     float *r;        // [npad]             rhs (residuals), solved in place
     float *dia;      // [npad]             velerr^2 + jit^2
     SC *tab;         // [kTabN]
@@ -73,9 +72,7 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
     {
         float *f = reinterpret_cast<float *>(smem_d);
         L.pan = f;
-        f += (npad - TB) * PS;
-        L.dg = f;
-        f += TB * PS;
+        f += (npad - TB) * TB;
         L.li = f;
         f += TB * PS;
         L.r = f;
@@ -131,64 +128,79 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
             L.dia[i] = di;
         }
         __syncthreads();
-        // ---- 2. covariance tiles (lower triangle) ----------------------------------------
+        // ---- 2. left-looking blocked Cholesky, covariance generated on the fly ------------
         const double amp = hp[0], lam_e = hp[1], lam_p = hp[2], per = hp[3];
         const float amp2 = (float)(amp * amp);
         const float gam = (float)(1.0 / (2.0 * lam_p * lam_p));   // gp.py:150
         const double inv_per = 1.0 / per, inv_le = 1.0 / lam_e;
-        const int ntiles = (RVK_GP_ABLATE & 4) ? 0 : nt * (nt + 1) / 2;
-        for (int t = wv; t < ntiles; t += kWavesPerBlock) {
-            int bi = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-            while (bi * (bi + 1) / 2 > t) --bi;
-            while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-            const int bj = t - bi * (bi + 1) / 2;
-            float *T = A + (long long)t * (TB * TB);
-            const int col = lane & 31, j = bj * TB + col;
-            const double tj = j < n ? d.t[j] : 0.0;
-#pragma unroll 4
-            for (int r = 0; r < 16; ++r) {
-                const int rr = cd_row(r, lane), i = bi * TB + rr;
-                float v;
-                if (i >= n || j >= n) {
-                    v = (i == j) ? 1.0f : 0.0f;
-                } else {
-                    const double tau = d.t[i] - tj;
-                    // sin^2(pi tau / P) from the phase reduced in fp64, then fp32
-                    const double ph = tau * inv_per;
-                    const float fr = (float)(ph - __builtin_rint(ph));
-                    const float s = __builtin_amdgcn_sinf(0.5f * fr);     // v_sin_f32 takes revolutions
-                    const float x = (float)(tau * inv_le);
-                    v = amp2 * __expf(-(gam * (s * s) + 0.5f * (x * x)));
-                    if (i == j) v += L.dia[i];
-                }
-                T[rr * TB + col] = v;
-            }
-        }
-        __syncthreads();
-        // ---- 3. blocked Cholesky with the rhs carried along ------------------------------
-        double logdet = 0.0, quad = 0.0;    // meaningful in thread 0
+        // C_ij (gp.py:126-156 + fit.py:8090-8105); padding is identity
+        auto cov = [&](int i, int j) -> float {
+            if (i >= n || j >= n) return (i == j) ? 1.0f : 0.0f;
+            const double tau = d.t[i] - d.t[j];
+            // sin^2(pi tau / P) from the phase reduced in fp64, then fp32
+            const double ph = tau * inv_per;
+            const float fr = (float)(ph - __builtin_rint(ph));
+            const float s = __builtin_amdgcn_sinf(0.5f * fr);     // v_sin_f32 takes revolutions
+            const float x = (float)(tau * inv_le);
+            float v = amp2 * __expf(-(gam * (s * s) + 0.5f * (x * x)));
+            if (i == j) v += L.dia[i];
+            return v;
+        };
+        double logdet = 0.0, quad = 0.0;    // meaningful in wave 0
         for (int kb = 0; kb < nt; ++kb) {
             // lane-derived addresses are recomputed per step, not hoisted and held for the kernel
             int ln = lane;
             asm volatile("" : "+v"(ln));
-            // a. diagonal tile (wave 0), in registers: lane i holds row i; the pivots and the
-            //    column entries other lanes need are broadcast with v_readlane (no LDS, no
-            //    barriers).  Then the block's rhs by forward substitution, and L_kk (+ the
-            //    reciprocals of its diagonal) to LDS for the panel.
+            const int h = ln >> 5, c = ln & 31;
+            const int m = nt - kb - 1;               // tiles below the diagonal
+            // a. Every tile (bi, kb), bi >= kb, is accumulated as its transpose in MFMA C/D
+            //    layout,  pre^T = C_(bi,kb)^T - sum_j L_(kb,j) L_(bi,j)^T  (16 MFMAs per j; both
+            //    operands are rows of finished L tiles, lane l reading row l & 31 at columns
+            //    16 (l >> 5) + ks).  Lane l then holds row (l & 31) of pre at the columns
+            //    cd_row(r, l): the A operand of the solve below, with K permuted the same way.
+            //    Wave 0 takes the diagonal tile, its rhs and its factorisation; waves 1..3 the
+            //    tiles below, parked in LDS for the solve.
+            auto accumulate = [&](int bi, f32x16 &acc, float &srhs, bool rhs) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = cov(bi * TB + c, kb * TB + cd_row(r, ln));
+                for (int j = 0; j < kb; ++j) {
+                    const float4 *pk4 = reinterpret_cast<const float4 *>(A + tile_index(kb, j) * (TB * TB) + c * TB + 16 * h);
+                    const float4 *pb4 = reinterpret_cast<const float4 *>(A + tile_index(bi, j) * (TB * TB) + c * TB + 16 * h);
+                    float ka[16], kbv[16];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 u = pk4[q], v = pb4[q];
+                        ka[4 * q] = u.x; ka[4 * q + 1] = u.y; ka[4 * q + 2] = u.z; ka[4 * q + 3] = u.w;
+                        kbv[4 * q] = v.x; kbv[4 * q + 1] = v.y; kbv[4 * q + 2] = v.z; kbv[4 * q + 3] = v.w;
+                    }
+#pragma unroll
+                    for (int ks = 0; ks < 16; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(-ka[ks], kbv[ks], acc, 0, 0, 0);
+                    if (rhs) {
+                        const float *yj = L.r + j * TB + 16 * h;
+#pragma unroll
+                        for (int ks = 0; ks < 16; ++ks) srhs = __builtin_fmaf(ka[ks], yj[ks], srhs);
+                    }
+                }
+            };
             if (wv == 0) {
-                const int i = ln & 31;
-                const float *src = A + tile_index(kb, kb) * (TB * TB) + i * TB;
+                f32x16 acc;
+                float srhs = 0.0f;
+                accumulate(kb, acc, srhs, true);
+                // b. factor the diagonal tile in registers: lane i (< 32) gathers row i (the
+                //    other half of its columns from lane i + 32; pre is symmetric), then
+                //    left-looking, one column per step r: row r of L (lane r's finished entries
+                //    L[r][k], k < r) is broadcast with v_readlane and shared by the column update
+                //    a_i[r] -= sum_k a_i[k] L[r][k], the rhs y_r and the inverse's row
+                //    X[r][j] = (delta_rj - sum_k L[r][k] X[k][j]) / L[r][r] (lane j = column j).
+                const int i = c;
                 float a[TB];
 #pragma unroll
-                for (int c = 0; c < TB; c += 4) {
-                    const float4 v = *reinterpret_cast<const float4 *>(src + c);
-                    a[c] = v.x; a[c + 1] = v.y; a[c + 2] = v.z; a[c + 3] = v.w;
+                for (int r = 0; r < 16; ++r) {
+                    a[cd_row(r, 0)] = acc[r];
+                    a[cd_row(r, 32)] = __shfl_xor(acc[r], 32);
                 }
-                const float rb = L.r[kb * TB + i];
-                // Left-looking, one column per step r: row r of L (lane r's finished entries
-                // L[r][k], k < r) is broadcast with v_readlane and shared by the column update
-                // a_i[r] -= sum_k a_i[k] L[r][k], the rhs y_r and the inverse's row
-                // X[r][j] = (delta_rj - sum_k L[r][k] X[k][j]) / L[r][r] (lane j = column j).
+                srhs += __shfl_xor(srhs, 32);
+                const float rb = L.r[kb * TB + i] - srhs;
                 float xinv[TB], y[TB];
                 double dprod = 1.0;                   // log det via products of 8 pivots
                 float yown = 0.0f;                    // y[i]
@@ -204,7 +216,7 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
                     }
                     const float dc = __builtin_sqrtf(rlf(col, r));    // not positive definite -> NaN
                     const float inv = 1.0f / dc;
-                    a[r] = (i == r) ? dc : col * inv;                 // rows i < r: upper part, unused
+                    a[r] = col * inv;                                 // rows i < r: upper part, unused
                     xinv[r] = xs * inv;
                     y[r] = ys * inv;
                     yown = (i == r) ? y[r] : yown;
@@ -215,81 +227,33 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
                     if ((r & 7) == 7) { logdet += log(dprod); dprod = 1.0; }
                 }
                 if (ln < TB) {
-#pragma unroll
-                    for (int c = 0; c < TB; ++c) L.dg[i * PS + c] = (c == i) ? 1.0f / a[c] : a[c];
                     L.r[kb * TB + i] = yown;
-                }
-                if (ln < TB) {
 #pragma unroll
-                    for (int r = 0; r < TB; ++r) L.li[r * PS + i] = xinv[r];   // Linv, row-major
+                    for (int r = 0; r < TB; ++r) L.li[r * PS + i] = xinv[r];   // L_kk^-1, row-major
+                }
+            } else {
+                for (int q = wv; q <= ((RVK_GP_ABLATE & 1) ? 0 : m); q += kWavesPerBlock - 1) {
+                    f32x16 acc;
+                    float unused = 0.0f;
+                    accumulate(kb + q, acc, unused, false);
+                    float *pre = L.pan + (q - 1) * (TB * TB);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) pre[r * 64 + ln] = acc[r];
                 }
             }
             __syncthreads();
-            const int m = nt - kb - 1;               // tiles below the diagonal
             if (m == 0) break;
-            // b. panel tiles P = A_(bi,kb) L_kk^-T with MFMA (16 per tile), waves over tiles, into
-            //    LDS; then the rhs below: r_i -= P_i . y (threads over rows)
-            for (int a = wv; a < ((RVK_GP_ABLATE & 2) ? 0 : m); a += kWavesPerBlock) {
-                // A operand: lane l holds A[l & 31][2 ks + (l >> 5)]
-                const float *src = A + tile_index(kb + 1 + a, kb) * (TB * TB) + (ln & 31) * TB + (ln >> 5);
-                float av[TB / 2];
-#pragma unroll
-                for (int ks = 0; ks < TB / 2; ++ks) av[ks] = src[2 * ks];
+            // c. L_(bi,kb) = pre L_kk^-T (16 MFMAs per tile): A = pre's rows as parked, B[k][j] =
+            //    L_kk^-1[j][k] at the permuted k; the C/D result is stored row-major.
+            for (int q = 1 + wv; q <= ((RVK_GP_ABLATE & 2) ? 0 : m); q += kWavesPerBlock) {
+                const float *pre = L.pan + (q - 1) * (TB * TB);
                 f32x16 acc = {};
-                const float *lb = L.li + (ln & 31) * PS + (ln >> 5);   // B[k][j] = Linv[j][k]
 #pragma unroll
-                for (int ks = 0; ks < TB / 2; ++ks)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ks], lb[2 * ks], acc, 0, 0, 0);
-                const int col = ln & 31;
+                for (int ks = 0; ks < 16; ++ks)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pre[ks * 64 + ln], L.li[c * PS + cd_row(ks, ln)], acc, 0, 0, 0);
+                float *T = A + tile_index(kb + q, kb) * (TB * TB);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) L.pan[(a * TB + cd_row(r, ln)) * PS + col] = acc[r];
-            }
-            __syncthreads();
-            for (int ri = tid; ri < m * TB; ri += kBlock) {
-                float acc = 0.0f;
-#pragma unroll
-                for (int c = 0; c < TB; ++c) acc = __builtin_fmaf(L.pan[ri * PS + c], L.r[kb * TB + c], acc);
-                L.r[(kb + 1) * TB + ri] -= acc;
-            }
-            __syncthreads();
-            // c. trailing update C -= P P^T on the lower triangle of tiles
-            const int cnt = (RVK_GP_ABLATE & 1) ? 0 : m * (m + 1) / 2;
-            const int col = ln & 31;
-            auto tile_of = [&](int t, int &a, int &b) {
-                a = (int)((__builtin_sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-                while (a * (a + 1) / 2 > t) --a;
-                while ((a + 1) * (a + 2) / 2 <= t) ++a;
-                b = t - a * (a + 1) / 2;                           // 0 <= b <= a < m
-            };
-            f32x16 cur;
-            int ta, tb;
-            if (wv < cnt) {
-                tile_of(wv, ta, tb);
-                const float *C = A + tile_index(kb + 1 + ta, kb + 1 + tb) * (TB * TB);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) cur[r] = C[cd_row(r, ln) * TB + col];
-            }
-            for (int t = wv; t < cnt; t += kWavesPerBlock) {
-                // the next tile's loads are in flight during this tile's MFMAs
-                f32x16 nxt;
-                int na = 0, nb2 = 0;
-                if (t + kWavesPerBlock < cnt) {
-                    tile_of(t + kWavesPerBlock, na, nb2);
-                    const float *Cn = A + tile_index(kb + 1 + na, kb + 1 + nb2) * (TB * TB);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) nxt[r] = Cn[cd_row(r, ln) * TB + col];
-                }
-                const float *pa = L.pan + (ta * TB + (ln & 31)) * PS + (ln >> 5);
-                const float *pb = L.pan + (tb * TB + (ln & 31)) * PS + (ln >> 5);
-#pragma unroll
-                for (int ks = 0; ks < TB / 2; ++ks)
-                    cur = __builtin_amdgcn_mfma_f32_32x32x2f32(-pa[2 * ks], pb[2 * ks], cur, 0, 0, 0);
-                float *C = A + tile_index(kb + 1 + ta, kb + 1 + tb) * (TB * TB);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) C[cd_row(r, ln) * TB + col] = cur[r];
-                cur = nxt;
-                ta = na;
-                tb = nb2;
+                for (int r = 0; r < 16; ++r) T[cd_row(r, ln) * TB + c] = acc[r];
             }
             __syncthreads();
         }
@@ -300,7 +264,7 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
 
 size_t gp_lds_bytes(int n, int np) {
     const int npad = ((n + TB - 1) / TB) * TB;
-    size_t b = sizeof(float) * ((size_t)(npad - TB) * PS + 2 * TB * PS + 2 * (size_t)npad) + 16;
+    size_t b = sizeof(float) * ((size_t)(npad - TB) * TB + TB * PS + 2 * (size_t)npad) + 16;
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
     return b;
 }

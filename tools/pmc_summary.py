@@ -8,21 +8,26 @@ import csv, glob, json, os, sys
 from collections import defaultdict
 
 out_dir, cfg = sys.argv[1], sys.argv[2]
+kfilter = sys.argv[3] if len(sys.argv) > 3 else None   # kernel-name substring (default: the plain loglike launch)
 vals = defaultdict(float)
 disp = defaultdict(set)
 kname = None
 for f in sorted(glob.glob(os.path.join(out_dir, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for row in csv.DictReader(open(f)):
         name = row.get("Kernel_Name", "")
-        if "loglike_kernel<" not in name or ", false>(" not in name:   # the plain (non-sampler) launch
+        if kfilter is not None:
+            if kfilter not in name:
+                continue
+        elif "loglike_kernel<" not in name or ", false>(" not in name:   # the plain (non-sampler) launch
             continue
         kname = name
         c = row["Counter_Name"]
         vals[c] += float(row["Counter_Value"])
         disp[c].add(row.get("Dispatch_Id", row.get("Correlation_Id")))
 per = {c: vals[c] / max(1, len(disp[c])) for c in vals}
-res = {"kernel": kname, "counters_per_launch": per,
-       "source": f"rocprofv3 --pmc passes over `python bench.py --config {cfg} --steps 20 --warmup 5 --no-cpu-baseline --no-sampler` (tools/pmc.sh)"}
+src = (f"rocprofv3 --pmc passes over `python tools/gp_bench.py` (tools/pmc_gp.sh)" if kfilter else
+       f"rocprofv3 --pmc passes over `python bench.py --config {cfg} --steps 20 --warmup 5 --no-cpu-baseline --no-sampler` (tools/pmc.sh)")
+res = {"kernel": kname, "counters_per_launch": per, "source": src}
 if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     res["hbm_bytes_per_launch"] = (2 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
 if "SQ_INSTS_VALU" in per:
