@@ -1,23 +1,35 @@
 // rvk_gp.hip -- batched quasi-periodic GP log-likelihood (include/rvk_gp.h;
 // SURVEY.md §8(f) row 2, BASELINE config 5).
 //
-// One workgroup (4 waves) per walker, grid-stride over walkers.  Per walker:
+// One workgroup of NW waves per walker (NW = 4 for n <= 512, 8 for n <= 1024),
+// grid-stride over walkers.  Per walker:
 //   1. planet constants (lanes over planets) and the mean model in fp64 (the
 //      log-likelihood kernel's Kepler solver, threads over epochs) -> residuals
 //      r and the diagonal velerr^2 + jit^2 in LDS (fp32);
-//   2. left-looking blocked Cholesky over 32-column steps kb with the right-hand
-//      side carried along (no triangular solve afterwards).  The covariance is
-//      never stored: each tile (bi, kb) is generated in registers when its step
-//      comes, and only the finished L tiles below the diagonal go to the
-//      walker's workspace (packed 32x32 tiles, fp32), read back by later steps:
-//        a. all waves: pre = C_(bi,kb) - sum_j L_(bi,j) L_(kb,j)^T with
-//           v_mfma_f32_32x32x2_f32 (wave 0 the diagonal tile and its rhs);
-//        b. wave 0 factors the diagonal tile in registers (v_readlane broadcasts),
-//           its rhs and inverse, log det and r^T C^-1 r in fp64;
-//        c. all waves: L_(bi,kb) = pre L_kk^-T with MFMA, stored.
-//   ll = -1/2 r^T C^-1 r - sum log L_ii - N/2 log(2 pi).
+//   2. blocked fp32 Cholesky over 32-wide tile columns k with the right-hand
+//      side carried along, pipelined one column ahead.  Tile row bi belongs to
+//      wave bi % NW for the whole factorisation; covariance tiles are generated
+//      in registers when first needed (never stored); finished L tiles go to
+//      the walker's workspace (packed 32x32 row-major tiles), the tiles of
+//      the column in flight are parked in LDS.  Step k:
+//        P(k)  wave k % NW factors the diagonal tile (registers; half the wave
+//              builds the rows of L_kk, the other half the columns of its
+//              inverse from the same v_readlane broadcasts), y_k = L_kk^-1 r_k;
+//              meanwhile every wave accumulates the NEXT column's tiles
+//              acc(bi, k+1) = C(bi, k+1) - sum_{j<k} L(bi, j) L(k+1, j)^T
+//              (v_mfma_f32_32x32x2_f32, in registers) -- the j = k term is
+//              the only part that waits for this step's factor;
+//        S1(k) every wave: L(bi, k) = acc(bi, k) L_kk^-T (MFMA), stored;
+//              r_bi -= L(bi, k) y_k;
+//        S2(k) every wave: acc(bi, k+1) -= L(bi, k) L(k+1, k)^T, parked for
+//              S1(k+1) (the diagonal tile stays in its owner's registers).
+//      Tiles are held transposed in MFMA C/D layout (lane l: row l & 31 of the
+//      tile at columns cd_row(r, l)), which is also the operand layout of the
+//      next product, so no tile is ever reshuffled.
+//   ll = -1/2 r^T C^-1 r - sum log L_ii - N/2 log(2 pi)  (fp64 sums).
 // Padding rows/columns up to a multiple of 32 are identity rows with r = 0.
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/rvk_gp.h"
@@ -27,14 +39,27 @@ using namespace rvk;
 
 namespace {
 
-#ifndef RVK_GP_ABLATE
-#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 no off-diagonal accumulation, 2 no solve
-#endif
 #ifndef RVK_GP_WGPCU
 #define RVK_GP_WGPCU 2    // concurrent workgroups per CU (each its own workspace), LDS permitting
 #endif
+#ifndef RVK_GP_ABLATE
+#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 part1 operands from LDS, 2 no factor
+#endif
+#ifndef RVK_GP_TRACE
+#define RVK_GP_TRACE 0    // timing experiments only: s_memtime per phase for the first walker of block 0
+#endif
+#if RVK_GP_TRACE
+__device__ unsigned long long g_gp_trace[8][32][8];
+#define GP_MARK(k, slot)                                                                          \
+    do {                                                                                          \
+        if (blockIdx.x == 0 && w == 0 && lane == 0) g_gp_trace[wv][k][slot] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define GP_MARK(k, slot) do {} while (0)
+#endif
 constexpr int TB = 32;              // tile edge
-constexpr int PS = TB + 1;          // LDS row stride of the panel / diagonal tile (bank spread)
+constexpr int TILE = TB * TB;
+constexpr int PS = TB + 1;          // LDS row stride of the diagonal inverse (bank spread)
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
@@ -42,7 +67,6 @@ __device__ __forceinline__ float rlf(float v, int lane) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
-__device__ __forceinline__ long long tile_index(int bi, int bj) { return (long long)bi * (bi + 1) / 2 + bj; }
 
 // MFMA 32x32 C/D map (cdna_hip_programming.md): register r of lane l holds
 // (row = (r & 3) + 8 (r >> 2) + 4 (l >> 5), col = l & 31).
@@ -50,49 +74,69 @@ __device__ __forceinline__ int cd_row(int r, int lane) { return (r & 3) + 8 * (r
 
 struct GpLds {
     // carved from dynamic shared memory
-    float *pan;      // [(npad - TB)][TB]  the step's tiles below the diagonal, before the solve
-    float *li;       // [TB][PS]           inverse of the step's diagonal tile
-    float *r;        // [npad]             rhs (residuals), solved in place
-    float *dia;      // [npad]             velerr^2 + jit^2
+    double *t;       // [npad]          epoch times (padding: copies of t[n-1])
+    float *pan;      // [nt - 1][TILE]  tile rows 1.. of the column in flight (C/D register order);
+                     //                 after S1(k) slot k holds L(k+1, k), read by every wave in S2(k)
+    float *li;       // [TB][PS]        inverse of the step's diagonal tile, row-major
+    float *r;        // [npad]          rhs (residuals), reduced in place
+    float *dia;      // [npad]          velerr^2 + jit^2
+    float *yk;       // [TB]            y_k = L_kk^-1 r_k
+    double *red;     // [3 NW]          per-wave partial sums
     SC *tab;         // [kTabN]
     PlanetK *pk;     // [NP]
     int *ok;         // [NP]
+    short *slot;     // [nt][nt]        workspace slot of tile (bi, j) (build_slots)
 };
 
-template <int NP, bool MULTI, bool TP>
-__global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int n, int ni,
-                                                           const double *__restrict__ theta,
-                                                           const double *__restrict__ hyper, long long W,
-                                                           long long stride, long long hstride,
-                                                           float *__restrict__ work, long long work_stride,
-                                                           double *__restrict__ out) {
+template <int NW>
+__device__ __forceinline__ GpLds carve(void *smem, int nt) {
+    GpLds L;
+    L.t = reinterpret_cast<double *>(smem);
+    float *f = reinterpret_cast<float *>(L.t + nt * TB);
+    L.pan = f;
+    f += (nt - 1) * TILE;
+    L.li = f;
+    f += TB * PS;
+    L.r = f;
+    f += nt * TB;
+    L.dia = f;
+    f += nt * TB;
+    L.yk = f;
+    f += TB;
+    L.red = reinterpret_cast<double *>(reinterpret_cast<uintptr_t>(f + 1) & ~uintptr_t(7));
+    L.tab = reinterpret_cast<SC *>(reinterpret_cast<uintptr_t>(L.red + 3 * NW + 1) & ~uintptr_t(15));
+    L.pk = reinterpret_cast<PlanetK *>(L.tab + kTabN);
+    L.ok = reinterpret_cast<int *>(L.pk + RVK_MAX_PLANETS);
+    L.slot = reinterpret_cast<short *>(L.ok + RVK_MAX_PLANETS);
+    return L;
+}
+
+template <bool MULTI, bool TP, int NW, int MAXR>   // MAXR tile rows per wave: nt <= MAXR * NW
+__global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kernel(EpochData d, int n, int ni, int np,
+                                                                             const double *__restrict__ theta,
+                                                                             const double *__restrict__ hyper,
+                                                                             long long W, long long stride,
+                                                                             long long hstride,
+                                                                             const short *__restrict__ slots,
+                                                                             float *__restrict__ work,
+                                                                             long long work_stride,
+                                                                             double *__restrict__ out) {
+    constexpr int NT = 64 * NW;
     extern __shared__ double smem_d[];
     const int nt = (n + TB - 1) / TB, npad = nt * TB;
-    GpLds L;
-    {
-        float *f = reinterpret_cast<float *>(smem_d);
-        L.pan = f;
-        f += (npad - TB) * TB;
-        L.li = f;
-        f += TB * PS;
-        L.r = f;
-        f += npad;
-        L.dia = f;
-        f += npad;
-        L.tab = reinterpret_cast<SC *>(reinterpret_cast<uintptr_t>(f + 3) & ~uintptr_t(15));
-        L.pk = reinterpret_cast<PlanetK *>(L.tab + kTabN);
-        L.ok = reinterpret_cast<int *>(L.pk + NP);
-    }
-    const int tid = threadIdx.x, lane = tid & 63;
+    const GpLds L = carve<NW>(smem_d, nt);
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < kTabN; i += kBlock) L.tab[i] = d.tab[i];
+    for (int i = tid; i < kTabN; i += NT) L.tab[i] = d.tab[i];
+    for (int i = tid; i < nt * TB; i += NT) L.t[i] = d.t[i < n ? i : n - 1];
+    for (int i = tid; i < nt * nt; i += NT) L.slot[i] = slots[i];
     float *A = work + (long long)blockIdx.x * work_stride;
 
     for (long long w = blockIdx.x; w < W; w += gridDim.x) {
         const double *row = theta + w * stride;
         const double *hp = hyper + w * hstride;
         // ---- 1. planets, mean model, residuals -------------------------------------------
-        if (tid < NP) {
+        if (tid < np) {
             PlanetK pk;
             const bool ok = TP ? planet_consts_t<0, true>(row + 5 * tid, pk, 0, L.tab)
                                : planet_consts(d.par, row + 5 * tid, pk);
@@ -101,23 +145,21 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
         }
         __syncthreads();   // (the table fill of the first trip lands here too)
         bool alive = true;
-#pragma unroll
-        for (int p = 0; p < NP; ++p) alive &= L.ok[p] != 0;
+        for (int p = 0; p < np; ++p) alive &= L.ok[p] != 0;
         if (!alive) {                                   // fit.py:8083-8085: mean model failed
             if (tid == 0) out[w] = -INFINITY;
             __syncthreads();
             continue;
         }
-        const double *g = row + 5 * NP, *jit = g + ni;
+        const double *g = row + 5 * np, *jit = g + ni;
         const double gd = jit[ni], gdd = jit[ni + 1];
-        for (int i = tid; i < npad; i += kBlock) {
+        for (int i = tid; i < npad; i += NT) {
             float ri = 0.0f, di = 1.0f;
             if (i < n) {
                 const double t = d.t[i];
                 const int ii = MULTI ? d.inst[i] : 0;
                 double rv = 0.0;
-#pragma unroll
-                for (int p = 0; p < NP; ++p) rv = planet_rv<0>(L.pk[p], t, L.tab, rv);
+                for (int p = 0; p < np; ++p) rv = planet_rv<0>(L.pk[p], t, L.tab, rv);
                 const double dt = t - d.t0;
                 rv += __builtin_fma(gd, dt, gdd * (dt * dt));      // Trend (fit.py:8031-8035)
                 rv += g[ii];                                       // gamma (fit.py:8041-8045)
@@ -128,182 +170,328 @@ __global__ __launch_bounds__(kBlock, 2) void gp_loglike_kernel(EpochData d, int 
             L.dia[i] = di;
         }
         __syncthreads();
-        // ---- 2. left-looking blocked Cholesky, covariance generated on the fly ------------
+        // ---- 2. pipelined blocked Cholesky ---------------------------------------------------
         const double amp = hp[0], lam_e = hp[1], lam_p = hp[2], per = hp[3];
-        const float amp2 = (float)(amp * amp);
+        const float namp2 = -(float)(amp * amp);
         const float gam = (float)(1.0 / (2.0 * lam_p * lam_p));   // gp.py:150
-        const double inv_per = 1.0 / per, inv_le = 1.0 / lam_e;
-        // C_ij (gp.py:126-156 + fit.py:8090-8105); padding is identity
-        auto cov = [&](int i, int j) -> float {
-            if (i >= n || j >= n) return (i == j) ? 1.0f : 0.0f;
-            const double tau = d.t[i] - d.t[j];
-            // sin^2(pi tau / P) from the phase reduced in fp64, then fp32
-            const double ph = tau * inv_per;
-            const float fr = (float)(ph - __builtin_rint(ph));
-            const float s = __builtin_amdgcn_sinf(0.5f * fr);     // v_sin_f32 takes revolutions
-            const float x = (float)(tau * inv_le);
-            float v = amp2 * __expf(-(gam * (s * s) + 0.5f * (x * x)));
-            if (i == j) v += L.dia[i];
-            return v;
-        };
-        double logdet = 0.0, quad = 0.0;    // meaningful in wave 0
-        for (int kb = 0; kb < nt; ++kb) {
-            // lane-derived addresses are recomputed per step, not hoisted and held for the kernel
-            int ln = lane;
-            asm volatile("" : "+v"(ln));
-            const int h = ln >> 5, c = ln & 31;
-            const int m = nt - kb - 1;               // tiles below the diagonal
-            // a. Every tile (bi, kb), bi >= kb, is accumulated as its transpose in MFMA C/D
-            //    layout,  pre^T = C_(bi,kb)^T - sum_j L_(kb,j) L_(bi,j)^T  (16 MFMAs per j; both
-            //    operands are rows of finished L tiles, lane l reading row l & 31 at columns
-            //    16 (l >> 5) + ks).  Lane l then holds row (l & 31) of pre at the columns
-            //    cd_row(r, l): the A operand of the solve below, with K permuted the same way.
-            //    Wave 0 takes the diagonal tile, its rhs and its factorisation; waves 1..3 the
-            //    tiles below, parked in LDS for the solve.
-            auto accumulate = [&](int bi, f32x16 &acc, float &srhs, bool rhs) {
+        const double inv_per = 1.0 / per;
+        // -C(bi, bj)^T in C/D layout: lane l, register r = -C[bi*32 + (l & 31)][bj*32 + cd_row(r, l)]
+        // (gp.py:126-156 + fit.py:8090-8105); padding rows/columns are identity.  Accumulators hold
+        // the NEGATED trailing tiles, -acc = -C + sum L L^T, so every MFMA adds (no sign flips).
+        const float inv_le = (float)(1.0 / lam_e);
+        auto cov_tile = [&](int bi, int bj, f32x16 &t) {
+            const double ti = L.t[bi * TB + c];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[r] = cov(bi * TB + c, kb * TB + cd_row(r, ln));
-                for (int j = 0; j < kb; ++j) {
-                    const float4 *pk4 = reinterpret_cast<const float4 *>(A + tile_index(kb, j) * (TB * TB) + c * TB + 16 * h);
-                    const float4 *pb4 = reinterpret_cast<const float4 *>(A + tile_index(bi, j) * (TB * TB) + c * TB + 16 * h);
-                    float ka[16], kbv[16];
+            for (int u = 0; u < 4; ++u) {
+                const double2 p0 = *reinterpret_cast<const double2 *>(L.t + bj * TB + 8 * u + 4 * h);
+                const double2 p1 = *reinterpret_cast<const double2 *>(L.t + bj * TB + 8 * u + 4 * h + 2);
+                const double tj[4] = {p0.x, p0.y, p1.x, p1.y};
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 u = pk4[q], v = pb4[q];
-                        ka[4 * q] = u.x; ka[4 * q + 1] = u.y; ka[4 * q + 2] = u.z; ka[4 * q + 3] = u.w;
-                        kbv[4 * q] = v.x; kbv[4 * q + 1] = v.y; kbv[4 * q + 2] = v.z; kbv[4 * q + 3] = v.w;
-                    }
-#pragma unroll
-                    for (int ks = 0; ks < 16; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(-ka[ks], kbv[ks], acc, 0, 0, 0);
-                    if (rhs) {
-                        const float *yj = L.r + j * TB + 16 * h;
-#pragma unroll
-                        for (int ks = 0; ks < 16; ++ks) srhs = __builtin_fmaf(ka[ks], yj[ks], srhs);
-                    }
+                for (int e = 0; e < 4; ++e) {
+                    const double tau = ti - tj[e];
+                    // sin^2(pi tau / P): the phase's fraction in fp64, then v_sin_f32 (revolutions)
+                    const float fr = (float)__builtin_amdgcn_fract(tau * inv_per);
+                    const float sn = __builtin_amdgcn_sinf(0.5f * fr);
+                    const float x = (float)tau * inv_le;
+                    t[4 * u + e] = namp2 * __expf(-(gam * (sn * sn) + 0.5f * (x * x)));
                 }
-            };
-            if (wv == 0) {
-                f32x16 acc;
-                float srhs = 0.0f;
-                accumulate(kb, acc, srhs, true);
-                // b. factor the diagonal tile in registers: lane i (< 32) gathers row i (the
-                //    other half of its columns from lane i + 32; pre is symmetric), then
-                //    left-looking, one column per step r: row r of L (lane r's finished entries
-                //    L[r][k], k < r) is broadcast with v_readlane and shared by the column update
-                //    a_i[r] -= sum_k a_i[k] L[r][k], the rhs y_r and the inverse's row
-                //    X[r][j] = (delta_rj - sum_k L[r][k] X[k][j]) / L[r][r] (lane j = column j).
-                const int i = c;
+            }
+            if (bi == bj || (bi + 1) * TB > n || (bj + 1) * TB > n) {
+                const int i = bi * TB + c;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int j = bj * TB + cd_row(r, lane);
+                    float v = (i < n && j < n) ? t[r] : 0.0f;
+                    v -= (i == j) ? L.dia[i] : 0.0f;                 // dia = 1 on padding
+                    t[r] = v;
+                }
+            }
+        };
+        double quad = 0.0;          // sum of y^2 over this wave's lanes
+        double dp = 1.0;            // product of this wave's pivots L_ii^2, renormalised (x 2^pexp)
+        int pexp = 0;
+        f32x16 nacc[MAXR], dacc;
+        // acc(bi, 0) = C(bi, 0): the diagonal tile in wave 0's registers, the rest parked
+#pragma unroll
+        for (int q = 0; q < MAXR; ++q) {
+            const int bi = wv + NW * q;
+            if (bi < nt) {
+                f32x16 t;
+                cov_tile(bi, 0, t);
+                if (bi == 0) {
+                    dacc = t;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) L.pan[(bi - 1) * TILE + r * 64 + lane] = t[r];
+                }
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < nt; ++k) {
+            GP_MARK(k, 0);
+            // ---- P(k): factor the diagonal tile (wave k % NW) --------------------------------
+#pragma unroll
+            for (int q = 0; q < MAXR; ++q) nacc[q] = f32x16{};   // (ends the previous step's live ranges)
+            if (wv == k % NW && !(RVK_GP_ABLATE & 2)) {
+                // lane i < 32: row i of acc(k,k) (half its columns from lane i + 32);
+                // lane 32 + j: column j of the identity, turned into column j of L_kk^-1
                 float a[TB];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    a[cd_row(r, 0)] = acc[r];
-                    a[cd_row(r, 32)] = __shfl_xor(acc[r], 32);
+                    const float o = __shfl_xor(dacc[r], 32);
+                    const int x0 = cd_row(r, 0), x1 = cd_row(r, 32);
+                    a[x0] = h ? (x0 == c ? 1.0f : 0.0f) : -dacc[r];
+                    a[x1] = h ? (x1 == c ? 1.0f : 0.0f) : -o;
                 }
-                srhs += __shfl_xor(srhs, 32);
-                const float rb = L.r[kb * TB + i] - srhs;
-                float xinv[TB], y[TB];
-                double dprod = 1.0;                   // log det via products of 8 pivots
-                float yown = 0.0f;                    // y[i]
+                // left-looking, one column per step r: L[r][k'] (lane r's finished a[k'])
+                // broadcast by v_readlane serves both halves:
+                //   rows:    a_i[r]  -= sum_k' a_i[k'] L[r][k'],   L[i][r] = a_i[r] / L[r][r]
+                //   inverse: X[r][j] = (delta_rj - sum_k' L[r][k'] X[k'][j]) / L[r][r]
 #pragma unroll
                 for (int r = 0; r < TB; ++r) {
-                    float col = a[r], xs = (r == i) ? 1.0f : 0.0f, ys = rlf(rb, r);
+                    int rr = r;                                      // opaque: this column's
+                    asm volatile("" : "+s"(rr));                     // broadcasts are not hoisted
+                    float v0 = a[r], v1 = 0.0f;
 #pragma unroll
-                    for (int k = 0; k < r; ++k) {
-                        const float lrk = rlf(a[k], r);
-                        col = __builtin_fmaf(-a[k], lrk, col);
-                        xs = __builtin_fmaf(-lrk, xinv[k], xs);
-                        ys = __builtin_fmaf(-lrk, y[k], ys);
+                    for (int kk = 0; kk < r; ++kk) {
+                        const float lrk = rlf(a[kk], rr);
+                        if (kk & 1) v1 = __builtin_fmaf(-a[kk], lrk, v1);
+                        else v0 = __builtin_fmaf(-a[kk], lrk, v0);
                     }
-                    const float dc = __builtin_sqrtf(rlf(col, r));    // not positive definite -> NaN
-                    const float inv = 1.0f / dc;
-                    a[r] = col * inv;                                 // rows i < r: upper part, unused
-                    xinv[r] = xs * inv;
-                    y[r] = ys * inv;
-                    yown = (i == r) ? y[r] : yown;
-                    asm volatile("" : "+v"(xinv[r]), "+v"(y[r]), "+v"(a[r]), "+v"(yown));   // finish step r here
-                    const bool live = kb * TB + r < n;
-                    dprod *= live ? (double)dc : 1.0;
-                    quad += live ? (double)y[r] * (double)y[r] : 0.0;
-                    if ((r & 7) == 7) { logdet += log(dprod); dprod = 1.0; }
+                    const float v = v0 + v1;
+                    const float p = rlf(v, rr);                      // L[r][r]^2 (<= 0 or NaN: NaN/inf
+                    a[r] = v * __builtin_amdgcn_rsqf(p);             //  propagate to y and the log)
+                    dp *= (double)p;
+                    asm volatile("" : "+v"(a[r]), "+v"(dp));        // column r finished here
+                    if ((r & 7) == 7) {
+                        int e;
+                        dp = __builtin_frexp(dp, &e);
+                        pexp += e;
+                    }
                 }
-                if (ln < TB) {
-                    L.r[kb * TB + i] = yown;
+                if (h) {
 #pragma unroll
-                    for (int r = 0; r < TB; ++r) L.li[r * PS + i] = xinv[r];   // L_kk^-1, row-major
+                    for (int r = 0; r < TB; ++r) L.li[r * PS + c] = -a[r];    // -X[r][c]
                 }
-            } else {
-                for (int q = wv; q <= ((RVK_GP_ABLATE & 1) ? 0 : m); q += kWavesPerBlock - 1) {
-                    f32x16 acc;
-                    float unused = 0.0f;
-                    accumulate(kb + q, acc, unused, false);
-                    float *pre = L.pan + (q - 1) * (TB * TB);
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                if (!h) {                                   // y_c = sum_j X[c][j] r_k[j]
+                    float y = 0.0f;
+                    const float *rk = L.r + k * TB;
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) pre[r * 64 + ln] = acc[r];
+                    for (int j = 0; j < TB; ++j) y = __builtin_fmaf(L.li[c * PS + j], rk[j], y);
+                    y = -y;
+                    L.yk[c] = y;
+                    quad += (double)y * (double)y;
                 }
             }
-            __syncthreads();
-            if (m == 0) break;
-            // c. L_(bi,kb) = pre L_kk^-T (16 MFMAs per tile): A = pre's rows as parked, B[k][j] =
-            //    L_kk^-1[j][k] at the permuted k; the C/D result is stored row-major.
-            for (int q = 1 + wv; q <= ((RVK_GP_ABLATE & 2) ? 0 : m); q += kWavesPerBlock) {
-                const float *pre = L.pan + (q - 1) * (TB * TB);
-                f32x16 acc = {};
+            GP_MARK(k, 1);
+            // ---- P(k): the next column's tiles, all but the j = k term ------------------------
+            if (k + 1 < nt) {
 #pragma unroll
-                for (int ks = 0; ks < 16; ++ks)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pre[ks * 64 + ln], L.li[c * PS + cd_row(ks, ln)], acc, 0, 0, 0);
-                float *T = A + tile_index(kb + q, kb) * (TB * TB);
+                for (int q = 0; q < MAXR; ++q) {
+                    const int bi = wv + NW * q;
+                    if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
+                }
+                // Per j: the A tile L(k+1, j) and every owned row's B tile L(bi, j) are loaded
+                // together (finished rows re-read the A tile, an L1 hit, so no load sits under a
+                // branch), then the MFMAs; the other workgroup on the CU hides the latency.
+                const long long lane_off = c * TB + 16 * h;
+                for (int j = 0; j < k; ++j) {
+                    float4 ta[4], tb[MAXR][4];
+                    const float4 *pa = reinterpret_cast<const float4 *>(A + L.slot[(k + 1) * nt + j] * TILE + lane_off);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) T[cd_row(r, ln) * TB + c] = acc[r];
+                    for (int u = 0; u < 4; ++u) ta[u] = pa[u];
+#pragma unroll
+                    for (int q = 0; q < MAXR; ++q) {
+                        const int bi = wv + NW * q;
+                        const bool live = bi >= k + 1 && bi < nt;
+                        const float4 *pb = reinterpret_cast<const float4 *>(
+                            A + L.slot[(live ? bi : k + 1) * nt + j] * TILE + lane_off);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) tb[q][u] = pb[u];
+                    }
+#pragma unroll
+                    for (int q = 0; q < MAXR; ++q) {
+                        const int bi = wv + NW * q;
+                        if (bi >= k + 1 && bi < nt) {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].x, tb[q][u].x, nacc[q], 0, 0, 0);
+                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].y, tb[q][u].y, nacc[q], 0, 0, 0);
+                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].z, tb[q][u].z, nacc[q], 0, 0, 0);
+                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].w, tb[q][u].w, nacc[q], 0, 0, 0);
+                            }
+                        }
+                    }
+                }
             }
-            __syncthreads();
+            GP_MARK(k, 2);
+            __syncthreads();                                // B1: L_kk^-1 and y_k published
+            GP_MARK(k, 3);
+            if (k + 1 == nt) break;
+            // ---- S1(k): L(bi, k) = acc(bi, k) L_kk^-T, stored; rhs update ---------------------
+            {
+                float ykv[16], la[16];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float4 x = *reinterpret_cast<const float4 *>(L.yk + 8 * u + 4 * h);
+                    ykv[4 * u] = x.x; ykv[4 * u + 1] = x.y; ykv[4 * u + 2] = x.z; ykv[4 * u + 3] = x.w;
+                }
+#pragma unroll
+                for (int ks = 0; ks < 16; ++ks) la[ks] = L.li[c * PS + cd_row(ks, lane)];
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q) {
+                    const int bi = wv + NW * q;
+                    if (bi > k && bi < nt) {
+                        float *slot = L.pan + (bi - 1) * TILE;
+                        float sb[16];
+#pragma unroll
+                        for (int ks = 0; ks < 16; ++ks) sb[ks] = slot[ks * 64 + lane];
+                        f32x16 lt = {};
+#pragma unroll
+                        for (int ks = 0; ks < 16; ++ks) lt = __builtin_amdgcn_mfma_f32_32x32x2f32(la[ks], sb[ks], lt, 0, 0, 0);
+                        // lane l: row c of L(bi, k) at columns cd_row(r, l) -> row-major tile
+                        // (L(k+1, k) is only ever read from LDS, in S2: not stored)
+                        float4 *T = reinterpret_cast<float4 *>(A + L.slot[bi * nt + k] * TILE + c * TB + 4 * h);
+                        float s = 0.0f;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (bi > k + 1) T[2 * u] = make_float4(lt[4 * u], lt[4 * u + 1], lt[4 * u + 2], lt[4 * u + 3]);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) s = __builtin_fmaf(lt[4 * u + e], ykv[4 * u + e], s);
+                        }
+                        s += __shfl_xor(s, 32);
+                        if (!h) L.r[bi * TB + c] -= s;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) slot[r * 64 + lane] = lt[r];   // L(k+1, k): read by all in S2
+                    }
+                }
+            }
+            GP_MARK(k, 4);
+            __syncthreads();                                // B2: L(k+1, k) published
+            GP_MARK(k, 5);
+            // ---- S2(k): the j = k term; park for S1(k+1) ---------------------------------------
+            float lk[16];
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) lk[ks] = L.pan[k * TILE + ks * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < MAXR; ++q) {
+                const int bi = wv + NW * q;
+                if (bi > k && bi < nt) {
+                    const float *src = L.pan + (bi - 1) * TILE;
+                    float sb[16];
+#pragma unroll
+                    for (int ks = 0; ks < 16; ++ks) sb[ks] = src[ks * 64 + lane];
+#pragma unroll
+                    for (int ks = 0; ks < 16; ++ks) nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(lk[ks], sb[ks], nacc[q], 0, 0, 0);
+                    if (bi == k + 1) {
+                        dacc = nacc[q];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) L.pan[(bi - 1) * TILE + r * 64 + lane] = nacc[q][r];
+                    }
+                }
+            }
+            GP_MARK(k, 6);
         }
-        if (tid == 0) out[w] = -0.5 * quad - logdet - 0.5 * (double)n * kLog2Pi;
+        // ---- 3. ll = -1/2 r^T C^-1 r - 1/2 sum log L_ii^2 - n/2 log 2 pi ------------------------
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) quad += __shfl_xor(quad, o);
+        if (lane == 0) {
+            L.red[3 * wv] = quad;
+            L.red[3 * wv + 1] = log(dp) + (double)pexp * 0.69314718055994530942;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double qs = 0.0, ls = 0.0;
+            for (int u = 0; u < NW; ++u) {
+                qs += L.red[3 * u];
+                ls += L.red[3 * u + 1];
+            }
+            const double ll = -0.5 * qs - 0.5 * ls - 0.5 * (double)n * kLog2Pi;
+            out[w] = __builtin_isfinite(ll) ? ll : NAN;     // not positive definite in fp32: NaN
+        }
         __syncthreads();
     }
 }
 
-size_t gp_lds_bytes(int n, int np) {
-    const int npad = ((n + TB - 1) / TB) * TB;
-    size_t b = sizeof(float) * ((size_t)(npad - TB) * TB + TB * PS + 2 * (size_t)npad) + 16;
-    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
+size_t gp_lds_bytes(int n, int np, int nw) {
+    const int nt = (n + TB - 1) / TB;
+    size_t b = sizeof(double) * (size_t)nt * TB;
+    b += sizeof(float) * ((size_t)(nt - 1) * TILE + TB * PS + 2 * (size_t)nt * TB + TB) + 16;
+    b += sizeof(double) * (3 * nw + 1) + 16;
+    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
+    b += sizeof(short) * (size_t)nt * nt;
+    (void)np;
     return b;
 }
 
-typedef void (*gp_launch_t)(hipStream_t, unsigned, size_t, EpochData, int, int, const double *, const double *,
-                            long long, long long, long long, float *, long long, double *);
+// Workspace slots.  Tile (bi, j), bi >= j + 2, is written in S1(j) and read in the P phases of
+// steps j + 1 .. bi - 1 (L(j + 1, j) never leaves LDS); a P-phase read precedes the same
+// step's S1 writes, so lifetimes [2j + 1, 2(bi - 1)] that do not overlap can share a slot.
+// Greedy interval colouring in order of first write: max_k (nt-1-k) k slots (56 at nt = 16)
+// instead of nt (nt - 1) / 2 (120), so concurrent walkers' workspaces stay in the Infinity Cache.
+int build_slots(int nt, std::vector<short> &slot) {
+    slot.assign((size_t)nt * nt, 0);
+    std::vector<int> free_at;            // per slot: the phase time after which it is free
+    for (int j = 0; j < nt; ++j)
+        for (int bi = j + 2; bi < nt; ++bi) {
+            const int start = 2 * j + 1, end = 2 * (bi - 1);
+            int s = -1;
+            for (size_t u = 0; u < free_at.size(); ++u)
+                if (free_at[u] < start) {
+                    s = (int)u;
+                    break;
+                }
+            if (s < 0) {
+                s = (int)free_at.size();
+                free_at.push_back(0);
+            }
+            free_at[s] = end;
+            slot[(size_t)bi * nt + j] = (short)s;
+        }
+    return (int)free_at.size();
+}
 
-template <int NP, bool MULTI, bool TP>
-void launch_gp(hipStream_t st, unsigned grid, size_t lds, EpochData d, int n, int ni, const double *th,
-               const double *hy, long long W, long long stride, long long hs, float *work, long long wstride,
-               double *out) {
+// launch shapes: waves per walker x tile rows per wave (nt <= NW * MAXR)
+struct GpShape {
+    int nw, maxr;
+};
+GpShape gp_shape(int n, int prefer_nw) {
+    const int nt = (n + TB - 1) / TB;
+    if (nt > 16) return {8, 4};
+    return prefer_nw == 8 ? GpShape{8, 2} : GpShape{4, 4};
+}
+
+typedef void (*gp_launch_t)(hipStream_t, unsigned, size_t, EpochData, int, int, int, const double *,
+                            const double *, long long, long long, long long, const short *, float *, long long,
+                            double *);
+
+template <bool MULTI, bool TP, int NW, int MAXR>
+void launch_gp(hipStream_t st, unsigned grid, size_t lds, EpochData d, int n, int ni, int np, const double *th,
+               const double *hy, long long W, long long stride, long long hs, const short *slots, float *work,
+               long long wstride, double *out) {
     static size_t allowed = 0;   // dynamic LDS beyond the default needs the attribute
     if (lds > allowed) {
-        (void)hipFuncSetAttribute((const void *)gp_loglike_kernel<NP, MULTI, TP>,
+        (void)hipFuncSetAttribute((const void *)gp_loglike_kernel<MULTI, TP, NW, MAXR>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         allowed = lds;
     }
-    hipLaunchKernelGGL((gp_loglike_kernel<NP, MULTI, TP>), dim3(grid), dim3(kBlock), lds, st, d, n, ni, th, hy, W,
-                       stride, hs, work, wstride, out);
+    hipLaunchKernelGGL((gp_loglike_kernel<MULTI, TP, NW, MAXR>), dim3(grid), dim3(64 * NW), lds, st, d, n, ni, np,
+                       th, hy, W, stride, hs, slots, work, wstride, out);
 }
 
-template <bool MULTI, bool TP>
-gp_launch_t pick_gp_s(int np) {
-    switch (np) {
-        case 1: return launch_gp<1, MULTI, TP>;
-        case 2: return launch_gp<2, MULTI, TP>;
-        case 3: return launch_gp<3, MULTI, TP>;
-        case 4: return launch_gp<4, MULTI, TP>;
-        case 5: return launch_gp<5, MULTI, TP>;
-        case 6: return launch_gp<6, MULTI, TP>;
-        case 7: return launch_gp<7, MULTI, TP>;
-        case 8: return launch_gp<8, MULTI, TP>;
-        default: return nullptr;
-    }
+template <int NW, int MAXR>
+gp_launch_t pick_gp_w(bool multi, bool tp) {
+    if (multi) return tp ? launch_gp<true, true, NW, MAXR> : launch_gp<true, false, NW, MAXR>;
+    return tp ? launch_gp<false, true, NW, MAXR> : launch_gp<false, false, NW, MAXR>;
 }
 
-gp_launch_t pick_gp(int np, bool multi, bool tp) {
-    if (multi) return tp ? pick_gp_s<true, true>(np) : pick_gp_s<true, false>(np);
-    return tp ? pick_gp_s<false, true>(np) : pick_gp_s<false, false>(np);
+gp_launch_t pick_gp(int np, bool multi, bool tp, GpShape sh) {
+    if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
+    if (sh.nw == 4) return pick_gp_w<4, 4>(multi, tp);
+    return sh.maxr == 2 ? pick_gp_w<8, 2>(multi, tp) : pick_gp_w<8, 4>(multi, tp);
 }
 
 }  // namespace
@@ -315,12 +503,14 @@ struct rvk_gp {
     size_t lds = 0;
     long long wstride = 0;       // floats per workgroup workspace
     float *d_work = nullptr;
+    short *d_slots = nullptr;    // [nt][nt] tile -> workspace slot
 };
 
 static void free_gp(rvk_gp *g) {
     if (!g) return;
     if (g->h) (void)hipSetDevice(g->h->device);
     (void)hipFree(g->d_work);
+    (void)hipFree(g->d_slots);
     delete g;
 }
 
@@ -329,21 +519,37 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     if (kernel != RVK_GP_QUASIPERIODIC) return fail(RVK_E_ARG, "unknown GP kernel type");
     if (h->n < 1 || h->n > RVK_GP_MAX_EPOCHS) return fail(RVK_E_ARG, "GP needs 1 <= n_epochs <= 1024");
     g->h = h;
-    g->launch = pick_gp(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP);
-    g->lds = gp_lds_bytes(h->n, h->n_planets);
+    // experiment hooks (tools/gp_ab.sh), never set in production: waves per walker, workgroups per CU
+    int wgpcu = RVK_GP_WGPCU, prefer_nw = 4;
+    if (const char *e = getenv("RVK_GP_NW")) prefer_nw = atoi(e);
+    if (const char *e = getenv("RVK_GP_WGPCU")) wgpcu = atoi(e) > 1 ? atoi(e) : 1;
+    const GpShape sh = gp_shape(h->n, prefer_nw);
+    g->launch = pick_gp(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, sh);
+    if (!g->launch) return fail(RVK_E_ARG, "GP supports 1..8 planets");
+    g->lds = gp_lds_bytes(h->n, h->n_planets, sh.nw);
     HIPCHK(hipSetDevice(h->device));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, h->device));
     // workgroups that fit at once (LDS-limited), each with its own workspace
     const size_t per_cu = (size_t)160 * 1024 / g->lds;
-    g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > RVK_GP_WGPCU ? RVK_GP_WGPCU : per_cu)));
+    g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > (size_t)wgpcu ? (size_t)wgpcu : per_cu)));
     const int nt = (h->n + TB - 1) / TB;
-    g->wstride = (long long)nt * (nt + 1) / 2 * TB * TB;
+    std::vector<short> slots;
+    const int nslots = build_slots(nt, slots);
+    g->wstride = (long long)(nslots > 0 ? nslots : 1) * TILE;
     HIPCHK(hipMalloc(&g->d_work, sizeof(float) * (size_t)g->wstride * g->grid));
+    HIPCHK(hipMalloc(&g->d_slots, sizeof(short) * slots.size()));
+    HIPCHK(hipMemcpy(g->d_slots, slots.data(), sizeof(short) * slots.size(), hipMemcpyHostToDevice));
     return RVK_OK;
 }
 
 extern "C" {
+
+#if RVK_GP_TRACE
+int rvk_gp_trace_dump(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gp_trace), sizeof(g_gp_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 rvk_gp *rvk_gp_create(rvk_handle *h, int32_t kernel_type) {
     rvk_gp *g = new (std::nothrow) rvk_gp();
@@ -369,8 +575,8 @@ int rvk_gp_loglike_device(rvk_gp *g, const double *d_theta, const double *d_hype
     if (!d_theta || !d_hyper || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     HIPCHK(hipSetDevice(h->device));
     const unsigned grid = (unsigned)((long long)g->grid < W ? g->grid : W);
-    g->launch((hipStream_t)stream, grid, g->lds, h->epochs(), h->n, h->n_inst, d_theta, d_hyper, W, stride, hstride,
-              g->d_work, g->wstride, d_out);
+    g->launch((hipStream_t)stream, grid, g->lds, h->epochs(), h->n, h->n_inst, h->n_planets, d_theta, d_hyper, W, stride,
+              hstride, g->d_slots, g->d_work, g->wstride, d_out);
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }
