@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TF = 78.6     # MI355X FP64 vector peak (spec; half the FP32 vector rate)
+FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
 BYTES_PER_WALKER_EPOCH = 28    # t, v, sigma fp64 + int32 inst
 
 
@@ -45,6 +46,7 @@ def parse():
     ap.add_argument("--no-sampler", action="store_true", help="skip the device stretch-move measurement")
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
     ap.add_argument("--streams", type=int, default=1, help="independent streams per graph")
+    ap.add_argument("--no-gp", action="store_true", help="skip the config-5 GP likelihood measurement")
     return ap.parse_args()
 
 
@@ -131,6 +133,51 @@ def sampler_line(W: int, steps: int = 256) -> dict:
     return {"what": f"device stretch move (rvk_stretch_run), config-2 posterior, {W} walkers, {D} free parameters, "
                     "Philox draws, chain in HBM", "ms_per_step": dev_ms, "walker_steps_per_s": W / (dev_ms * 1e-3),
             "acceptance": acc, "host_stretch_move_ms_per_step": host_ms, "speedup_vs_host": host_ms / dev_ms}
+
+
+def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
+    """Config 5: batched quasi-periodic GP log-likelihood, 1 planet, 512
+    epochs, 4096 walkers, fp32 factorisation (rvk_gp_loglike_device), theta/hyper resident in
+    HBM; HIP events around `reps` back-to-back launches on the launch stream.  Roofline: fp32
+    MFMA, algorithmic FLOP per walker = n^3/3 (Cholesky) + 2 n^2 (the carried rhs).  CPU
+    baseline: the fp64 restatement (oracle/gp_oracle.py, scipy Cholesky), one BLAS thread."""
+    import torch
+    from ravest_amd.gp import GPKernel, GPLogLikelihood
+    from ravest_amd.synth import make_gp_config
+    ds, th, hy = make_gp_config(W, n_epochs=n)
+    gp = GPLogLikelihood(ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments, ds.planet_letters,
+                         ds.parameterisation, GPKernel("Quasiperiodic"), device=torch.cuda.current_device())
+    dev = torch.device("cuda", torch.cuda.current_device())
+    tt, ht = torch.from_numpy(th).to(dev), torch.from_numpy(hy).to(dev)
+    out = torch.empty(W, dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    for _ in range(2):
+        gp.device(tt, ht, out, st)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
+        gp.device(tt, ht, out, st)
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    ms = a.elapsed_time(b) / reps
+    flop = W * (n ** 3 / 3.0 + 2.0 * n * n)
+    tf = flop / (ms * 1e-3) / 1e12
+    from threadpoolctl import threadpool_limits
+    from oracle import gp_oracle
+    k = 24
+    with threadpool_limits(1):
+        gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:2], hy[:2])
+        t0 = time.perf_counter()
+        gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:k], hy[:k])
+        cpu_s = (time.perf_counter() - t0) / k
+    return {"config": f"config 5: 1 planet + quasi-periodic GP, {n} epochs, {W} walkers, fp32 factorisation",
+            "ms_per_eval": ms, "walker_evals_per_s": W / (ms * 1e-3),
+            "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                         "frac": tf / FP32_MFMA_PEAK_TF, "traffic": None,
+                         "note": "algorithmic FLOP = W*(n^3/3 + 2n^2) per launch / launch duration"},
+            "n_masked_walkers": int((~np.isfinite(out.cpu().numpy())).sum()),
+            "cpu_baseline": {"value": 1.0 / cpu_s, "unit": "walker evals/s", "cores": 1, "kind": "port",
+                             "sample": f"{k} walkers, fp64 restatement (oracle/gp_oracle.py, scipy LAPACK, 1 thread)"}}
 
 
 def main():
@@ -309,6 +356,8 @@ def main():
         line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
         if world == 1 and not args.no_sampler:
             line["sampler"] = sampler_line(W)
+        if world == 1 and not args.no_gp:
+            line["gp_config5"] = gp_line()
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -30,6 +30,7 @@
 // Padding rows/columns up to a multiple of 32 are identity rows with r = 0.
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rvk_gp.h"
@@ -44,6 +45,12 @@ namespace {
 #endif
 #ifndef RVK_GP_ABLATE
 #define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 part1 operands from LDS, 2 no factor
+#endif
+#ifndef RVK_GP_PRIO
+#define RVK_GP_PRIO 1     // s_setprio of the factoring wave (1 and 3 measured equal, 0 within noise)
+#endif
+#ifndef RVK_GP_AGPR
+#define RVK_GP_AGPR 0     // accumulators in AGPRs (MFMA C/D off the VGPR file)
 #endif
 #ifndef RVK_GP_TRACE
 #define RVK_GP_TRACE 0    // timing experiments only: s_memtime per phase for the first walker of block 0
@@ -103,8 +110,12 @@ __device__ __forceinline__ GpLds carve(void *smem, int nt) {
     f += nt * TB;
     L.yk = f;
     f += TB;
-    L.red = reinterpret_cast<double *>(reinterpret_cast<uintptr_t>(f + 1) & ~uintptr_t(7));
-    L.tab = reinterpret_cast<SC *>(reinterpret_cast<uintptr_t>(L.red + 3 * NW + 1) & ~uintptr_t(15));
+    // every offset so far is a multiple of 16 bytes; plain pointer arithmetic on the shared
+    // base (no integer casts) keeps these LDS pointers: integer casts would turn every access
+    // into a flat one, which waits on vmcnt as well
+    L.red = reinterpret_cast<double *>(f);
+    static_assert((3 * NW * sizeof(double)) % 16 == 0, "table alignment");
+    L.tab = reinterpret_cast<SC *>(L.red + 3 * NW);
     L.pk = reinterpret_cast<PlanetK *>(L.tab + kTabN);
     L.ok = reinterpret_cast<int *>(L.pk + RVK_MAX_PLANETS);
     L.slot = reinterpret_cast<short *>(L.ok + RVK_MAX_PLANETS);
@@ -127,6 +138,19 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
     const GpLds L = carve<NW>(smem_d, nt);
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // Tile rows are owned round-robin by waves, rotated per workgroup: in the last steps only one
+    // or two rows are left, and workgroups sharing a CU then keep different SIMDs busy.
+#ifndef RVK_GP_ROT
+#define RVK_GP_ROT 1
+#endif
+    const int rot = RVK_GP_ROT ? (int)((blockIdx.x * 7u + (blockIdx.x >> 8)) % NW) : 0;
+    const int wr = (wv - rot + NW) % NW;    // this wave owns tile rows wr, wr + NW, ...
+#if RVK_GP_AGPR
+    {   // an AGPR operand anywhere makes the compiler select the AGPR form of every MFMA
+        float z = 0.0f;
+        asm volatile("; agpr hint %0" : "+a"(z));
+    }
+#endif
     for (int i = tid; i < kTabN; i += NT) L.tab[i] = d.tab[i];
     for (int i = tid; i < nt * TB; i += NT) L.t[i] = d.t[i < n ? i : n - 1];
     for (int i = tid; i < nt * nt; i += NT) L.slot[i] = slots[i];
@@ -214,7 +238,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
         // acc(bi, 0) = C(bi, 0): the diagonal tile in wave 0's registers, the rest parked
 #pragma unroll
         for (int q = 0; q < MAXR; ++q) {
-            const int bi = wv + NW * q;
+            const int bi = wr + NW * q;
             if (bi < nt) {
                 f32x16 t;
                 cov_tile(bi, 0, t);
@@ -232,7 +256,10 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             // ---- P(k): factor the diagonal tile (wave k % NW) --------------------------------
 #pragma unroll
             for (int q = 0; q < MAXR; ++q) nacc[q] = f32x16{};   // (ends the previous step's live ranges)
-            if (wv == k % NW && !(RVK_GP_ABLATE & 2)) {
+            if (wr == k % NW && !(RVK_GP_ABLATE & 2)) {
+                // the factor is the step's critical path: its VALU chain goes ahead of the
+                // co-resident waves' instructions (MI355X_MICROARCH.md, two waves per SIMD)
+                __builtin_amdgcn_s_setprio(RVK_GP_PRIO);
                 // lane i < 32: row i of acc(k,k) (half its columns from lane i + 32);
                 // lane 32 + j: column j of the identity, turned into column j of L_kk^-1
                 float a[TB];
@@ -284,47 +311,76 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                     L.yk[c] = y;
                     quad += (double)y * (double)y;
                 }
+                __builtin_amdgcn_s_setprio(0);
             }
             GP_MARK(k, 1);
             // ---- P(k): the next column's tiles, all but the j = k term ------------------------
             if (k + 1 < nt) {
 #pragma unroll
                 for (int q = 0; q < MAXR; ++q) {
-                    const int bi = wv + NW * q;
+                    const int bi = wr + NW * q;
                     if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
                 }
-                // Per j: the A tile L(k+1, j) and every owned row's B tile L(bi, j) are loaded
-                // together (finished rows re-read the A tile, an L1 hit, so no load sits under a
-                // branch), then the MFMAs; the other workgroup on the CU hides the latency.
+                // Operand tiles: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows
+                // at a time (rows q0, q0 + 1; a second pass takes rows 2, 3 and re-reads the A
+                // tiles from L2).  Two register sets X / Y alternate over j (the loop is unrolled
+                // by two), so the next j's tiles are in flight during this j's MFMAs.  Finished
+                // rows (and the trip past the end) re-read the A tile, an L1 hit, so every load
+                // is unconditional and every path through the loop leaves the same loads
+                // outstanding (exact s_waitcnt vmcnt).
                 const long long lane_off = c * TB + 16 * h;
-                for (int j = 0; j < k; ++j) {
-                    float4 ta[4], tb[MAXR][4];
-                    const float4 *pa = reinterpret_cast<const float4 *>(A + L.slot[(k + 1) * nt + j] * TILE + lane_off);
+                auto pass = [&](auto q0c) {
+                    constexpr int Q0 = decltype(q0c)::value;
+                    constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
+                    bool any = false;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) ta[u] = pa[u];
+                    for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NW * q >= k + 1) && (wr + NW * q < nt);
+                    if (!any || k == 0) return;
+                    struct Ops {
+                        float4 a[4], b[R][4];
+                    };
+                    auto issue = [&](Ops &o, int j) {
+                        const int jj = j < k ? j : k - 1;
+                        const float4 *pa = reinterpret_cast<const float4 *>(A + L.slot[(k + 1) * nt + jj] * TILE + lane_off);
 #pragma unroll
-                    for (int q = 0; q < MAXR; ++q) {
-                        const int bi = wv + NW * q;
-                        const bool live = bi >= k + 1 && bi < nt;
-                        const float4 *pb = reinterpret_cast<const float4 *>(
-                            A + L.slot[(live ? bi : k + 1) * nt + j] * TILE + lane_off);
+                        for (int u = 0; u < 4; ++u) o.a[u] = pa[u];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) tb[q][u] = pb[u];
-                    }
+                        for (int q = 0; q < R; ++q) {
+                            const int bi = wr + NW * (Q0 + q);
+                            const bool live = bi >= k + 1 && bi < nt;
+                            const float4 *pb = reinterpret_cast<const float4 *>(
+                                A + L.slot[(live ? bi : k + 1) * nt + jj] * TILE + lane_off);
 #pragma unroll
-                    for (int q = 0; q < MAXR; ++q) {
-                        const int bi = wv + NW * q;
-                        if (bi >= k + 1 && bi < nt) {
+                            for (int u = 0; u < 4; ++u) o.b[q][u] = pb[u];
+                        }
+                    };
+                    auto consume = [&](const Ops &o) {
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].x, tb[q][u].x, nacc[q], 0, 0, 0);
-                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].y, tb[q][u].y, nacc[q], 0, 0, 0);
-                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].z, tb[q][u].z, nacc[q], 0, 0, 0);
-                                nacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ta[u].w, tb[q][u].w, nacc[q], 0, 0, 0);
+                        for (int q = 0; q < R; ++q) {
+                            const int bi = wr + NW * (Q0 + q);
+                            if (bi >= k + 1 && bi < nt) {
+                                f32x16 &acc = nacc[Q0 + q];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].x, o.b[q][u].x, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].y, o.b[q][u].y, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].z, o.b[q][u].z, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].w, o.b[q][u].w, acc, 0, 0, 0);
+                                }
                             }
                         }
+                    };
+                    Ops X, Y;
+                    issue(X, 0);
+                    for (int j = 0; j < k; j += 2) {
+                        issue(Y, j + 1);
+                        consume(X);
+                        issue(X, j + 2);
+                        if (j + 1 < k) consume(Y);
                     }
-                }
+                };
+                pass(std::integral_constant<int, 0>{});
+                if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
             }
             GP_MARK(k, 2);
             __syncthreads();                                // B1: L_kk^-1 and y_k published
@@ -342,7 +398,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 for (int ks = 0; ks < 16; ++ks) la[ks] = L.li[c * PS + cd_row(ks, lane)];
 #pragma unroll
                 for (int q = 0; q < MAXR; ++q) {
-                    const int bi = wv + NW * q;
+                    const int bi = wr + NW * q;
                     if (bi > k && bi < nt) {
                         float *slot = L.pan + (bi - 1) * TILE;
                         float sb[16];
@@ -377,7 +433,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             for (int ks = 0; ks < 16; ++ks) lk[ks] = L.pan[k * TILE + ks * 64 + lane];
 #pragma unroll
             for (int q = 0; q < MAXR; ++q) {
-                const int bi = wv + NW * q;
+                const int bi = wr + NW * q;
                 if (bi > k && bi < nt) {
                     const float *src = L.pan + (bi - 1) * TILE;
                     float sb[16];
@@ -420,7 +476,7 @@ size_t gp_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * (size_t)nt * TB;
     b += sizeof(float) * ((size_t)(nt - 1) * TILE + TB * PS + 2 * (size_t)nt * TB + TB) + 16;
-    b += sizeof(double) * (3 * nw + 1) + 16;
+    b += sizeof(double) * 3 * nw;
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
     b += sizeof(short) * (size_t)nt * nt;
     (void)np;
