@@ -173,8 +173,10 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     return {"config": f"config 5: 1 planet + quasi-periodic GP, {n} epochs, {W} walkers, fp32 factorisation",
             "ms_per_eval": ms, "walker_evals_per_s": W / (ms * 1e-3),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                         "frac": tf / FP32_MFMA_PEAK_TF, "traffic": None,
-                         "note": "algorithmic FLOP = W*(n^3/3 + 2n^2) per launch / launch duration"},
+                         "frac": tf / FP32_MFMA_PEAK_TF, "traffic": (load_pmc(5) or {}).get("hbm_bytes_per_launch"),
+                         "note": "algorithmic FLOP = W*(n^3/3 + 2n^2) per launch / launch duration; traffic = "
+                                 "L2 memory-side bytes per launch (PMC, profiles/pmc_config5.json; includes "
+                                 "Infinity-Cache hits: the workspace tiles re-read by the left-looking update)"},
             "n_masked_walkers": int((~np.isfinite(out.cpu().numpy())).sum()),
             "cpu_baseline": {"value": 1.0 / cpu_s, "unit": "walker evals/s", "cores": 1, "kind": "port",
                              "sample": f"{k} walkers, fp64 restatement (oracle/gp_oracle.py, scipy LAPACK, 1 thread)"}}
