@@ -31,7 +31,11 @@ def _gp(ds, n_inst=1):
 
 @pytest.mark.parametrize("n,np_,ni,par,trend", [(512, 1, 1, "P K e w Tp", False), (100, 1, 2, "P K e w Tc", True),
                                                 (37, 2, 1, "P K secosw sesinw Tp", False),
-                                                (300, 3, 3, "P K e w Tp", True)])
+                                                (300, 3, 3, "P K e w Tp", True),
+                                                (32, 1, 1, "P K e w Tp", False),            # one tile
+                                                (33, 1, 1, "P K e w Tp", False),            # one row of padding tiles
+                                                (700, 1, 1, "P K e w Tp", False),           # 8-wave shape
+                                                (1024, 2, 2, "P K secosw sesinw Tc", True)])  # maximum size
 def test_gp_loglike_vs_fp64_oracle(n, np_, ni, par, trend):
     from oracle import gp_oracle
     from ravest_amd.synth import make_dataset, make_walkers
@@ -91,3 +95,19 @@ def test_gp_reference_fixture_values():
     assert abs(got - ref) <= 1e-5 * abs(ref) + 1e-4
     bad = dict(params, P_b=-1.0)                 # tests/test_fit.py:1577-1600: invalid planet -> -inf
     assert ll(bad, hyper) == -np.inf
+
+
+def test_gp_narrow_shape_matches(monkeypatch):
+    """The 8-waves x 2-rows launch shape (experiment hook RVK_GP_NW=8) gives the same values as
+    the default 4 x 4 shape up to fp32 summation order, and passes the oracle tolerance."""
+    from oracle import gp_oracle
+    from ravest_amd.synth import make_gp_config
+    ds, th, hy = make_gp_config(64)
+    base = _gp(ds).batch(th, hy)
+    monkeypatch.setenv("RVK_GP_NW", "8")
+    narrow = _gp(ds).batch(th, hy)
+    assert np.array_equal(np.isfinite(base), np.isfinite(narrow))
+    fin = np.isfinite(base)
+    assert np.max(np.abs(base[fin] - narrow[fin]) / np.abs(base[fin])) < 1e-4
+    ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:16], hy[:16])
+    _check(narrow[:16], ref, "narrow")
