@@ -560,13 +560,29 @@ struct rvk_gp {
     long long wstride = 0;       // floats per workgroup workspace
     float *d_work = nullptr;
     short *d_slots = nullptr;    // [nt][nt] tile -> workspace slot
+    // host-buffer path (rvk_gp_loglike): device copies kept across calls, grown on demand
+    double *d_theta = nullptr, *d_hyper = nullptr, *d_out = nullptr;
+    size_t cap_theta = 0, cap_hyper = 0, cap_out = 0;
 };
+
+static int gp_grow(double **p, size_t *cap, size_t need) {
+    if (need <= *cap) return RVK_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need));
+    *cap = need;
+    return RVK_OK;
+}
 
 static void free_gp(rvk_gp *g) {
     if (!g) return;
     if (g->h) (void)hipSetDevice(g->h->device);
     (void)hipFree(g->d_work);
     (void)hipFree(g->d_slots);
+    (void)hipFree(g->d_theta);
+    (void)hipFree(g->d_hyper);
+    (void)hipFree(g->d_out);
     delete g;
 }
 
@@ -643,25 +659,19 @@ int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t 
     if (W == 0) return RVK_OK;
     if (!theta || !hyper || !out || W < 0) return fail(RVK_E_ARG, "bad host buffers");
     rvk_handle *h = g->h;
+    if (stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad walker block shape");
     HIPCHK(hipSetDevice(h->device));
-    double *dt = nullptr, *dh = nullptr, *dout = nullptr;
     const size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bh = sizeof(double) * (size_t)W * (size_t)hstride;
-    int rc = RVK_OK;
-    if (hipMalloc(&dt, bt) != hipSuccess || hipMalloc(&dh, bh) != hipSuccess ||
-        hipMalloc(&dout, sizeof(double) * (size_t)W) != hipSuccess)
-        rc = fail(RVK_E_HIP, "hipMalloc failed");
-    if (rc == RVK_OK && (hipMemcpyAsync(dt, theta, bt, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
-                         hipMemcpyAsync(dh, hyper, bh, hipMemcpyHostToDevice, h->stream) != hipSuccess))
-        rc = fail(RVK_E_HIP, "hipMemcpyAsync H2D failed");
-    if (rc == RVK_OK) rc = rvk_gp_loglike_device(g, dt, dh, W, stride, hstride, dout, h->stream);
-    if (rc == RVK_OK &&
-        hipMemcpyAsync(out, dout, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-        rc = fail(RVK_E_HIP, "hipMemcpyAsync D2H failed");
-    if (hipStreamSynchronize(h->stream) != hipSuccess && rc == RVK_OK) rc = fail(RVK_E_HIP, "stream sync failed");
-    (void)hipFree(dt);
-    (void)hipFree(dh);
-    (void)hipFree(dout);
-    return rc;
+    int rc;
+    if ((rc = gp_grow(&g->d_theta, &g->cap_theta, bt)) || (rc = gp_grow(&g->d_hyper, &g->cap_hyper, bh)) ||
+        (rc = gp_grow(&g->d_out, &g->cap_out, sizeof(double) * (size_t)W)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(g->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(g->d_hyper, hyper, bh, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_gp_loglike_device(g, g->d_theta, g->d_hyper, W, stride, hstride, g->d_out, h->stream))) return rc;
+    HIPCHK(hipMemcpyAsync(out, g->d_out, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RVK_OK;
 }
 
 }  // extern "C"
