@@ -52,11 +52,15 @@ namespace {
 #ifndef RVK_GP_AGPR
 #define RVK_GP_AGPR 0     // accumulators in AGPRs (MFMA C/D off the VGPR file)
 #endif
+#ifndef RVK_GP_FACTOR_LDS
+#define RVK_GP_FACTOR_LDS 0   // diagonal factor: row broadcasts through LDS (1) or v_readlane (0); measured equal
+#endif
 #ifndef RVK_GP_TRACE
 #define RVK_GP_TRACE 0    // timing experiments only: s_memtime per phase for the first walker of block 0
 #endif
 #if RVK_GP_TRACE
 __device__ unsigned long long g_gp_trace[8][32][8];
+#define GP_HWID() (__builtin_amdgcn_s_getreg((31 << 11) | 4))   // HW_REG_HW_ID: wave, SIMD, CU ids
 #define GP_MARK(k, slot)                                                                          \
     do {                                                                                          \
         if (blockIdx.x == 0 && w == 0 && lane == 0) g_gp_trace[wv][k][slot] = __builtin_amdgcn_s_memtime(); \
@@ -67,6 +71,8 @@ __device__ unsigned long long g_gp_trace[8][32][8];
 constexpr int TB = 32;              // tile edge
 constexpr int TILE = TB * TB;
 constexpr int PS = TB + 1;          // LDS row stride of the diagonal inverse (bank spread)
+constexpr int RS = TB + 4;          // row stride of the factor's row buffer (b128-aligned rows), same LDS
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
@@ -84,7 +90,8 @@ struct GpLds {
     double *t;       // [npad]          epoch times (padding: copies of t[n-1])
     float *pan;      // [nt - 1][TILE]  tile rows 1.. of the column in flight (C/D register order);
                      //                 after S1(k) slot k holds L(k+1, k), read by every wave in S2(k)
-    float *li;       // [TB][PS]        inverse of the step's diagonal tile, row-major
+    float *li;       // [TB][RS]        inverse of the step's diagonal tile, row-major (stride PS);
+                     //                 the factor's row buffer (stride RS) while it runs
     float *r;        // [npad]          rhs (residuals), reduced in place
     float *dia;      // [npad]          velerr^2 + jit^2
     float *yk;       // [TB]            y_k = L_kk^-1 r_k
@@ -103,7 +110,7 @@ __device__ __forceinline__ GpLds carve(void *smem, int nt) {
     L.pan = f;
     f += (nt - 1) * TILE;
     L.li = f;
-    f += TB * PS;
+    f += TB * RS;
     L.r = f;
     f += nt * TB;
     L.dia = f;
@@ -251,6 +258,9 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             }
         }
         __syncthreads();
+#if RVK_GP_TRACE
+        if (blockIdx.x == 0 && w == 0 && lane == 0) g_gp_trace[wv][31][7] = GP_HWID();
+#endif
         for (int k = 0; k < nt; ++k) {
             GP_MARK(k, 0);
             // ---- P(k): factor the diagonal tile (wave k % NW) --------------------------------
@@ -274,10 +284,38 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 // broadcast by v_readlane serves both halves:
                 //   rows:    a_i[r]  -= sum_k' a_i[k'] L[r][k'],   L[i][r] = a_i[r] / L[r][r]
                 //   inverse: X[r][j] = (delta_rj - sum_k' L[r][k'] X[k'][j]) / L[r][r]
+#if RVK_GP_FACTOR_LDS
+                // Row r of L (L[r][0..r-1]) reaches every lane through LDS instead of r
+                // v_readlane: each finished column is written once (lane i: L[i][c'] at
+                // rb[i][c'], row stride RS), row r is read back as uniform-address b128
+                // broadcasts, and pairs of terms go through v_pk_fma_f32.  li is free here
+                // (S1 of the previous step is behind the last barrier) and is rewritten
+                // with the inverse afterwards.
+                float *rb = L.li;
+#endif
 #pragma unroll
                 for (int r = 0; r < TB; ++r) {
                     int rr = r;                                      // opaque: this column's
                     asm volatile("" : "+s"(rr));                     // broadcasts are not hoisted
+#if RVK_GP_FACTOR_LDS
+                    if (r > 0 && !h) rb[c * RS + (r - 1)] = a[r - 1];   // publish column r - 1
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    float lr[TB];
+#pragma unroll
+                    for (int m = 0; m < (r + 3) / 4; ++m) {
+                        const float4 x = *reinterpret_cast<const float4 *>(rb + rr * RS + 4 * m);
+                        lr[4 * m] = x.x; lr[4 * m + 1] = x.y; lr[4 * m + 2] = x.z; lr[4 * m + 3] = x.w;
+                    }
+                    f32x2 acc2 = {a[r], 0.0f};
+#pragma unroll
+                    for (int kk = 0; kk + 1 < r; kk += 2) {
+                        const f32x2 av = {a[kk], a[kk + 1]}, lv = {lr[kk], lr[kk + 1]};
+                        acc2 = acc2 - av * lv;
+                    }
+                    if (r & 1) acc2.x = __builtin_fmaf(-a[r - 1], lr[r - 1], acc2.x);
+                    const float v = acc2.x + acc2.y;
+#else
                     float v0 = a[r], v1 = 0.0f;
 #pragma unroll
                     for (int kk = 0; kk < r; ++kk) {
@@ -286,6 +324,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                         else v0 = __builtin_fmaf(-a[kk], lrk, v0);
                     }
                     const float v = v0 + v1;
+#endif
                     const float p = rlf(v, rr);                      // L[r][r]^2 (<= 0 or NaN: NaN/inf
                     a[r] = v * __builtin_amdgcn_rsqf(p);             //  propagate to y and the log)
                     dp *= (double)p;
@@ -296,6 +335,10 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                         pexp += e;
                     }
                 }
+#if RVK_GP_FACTOR_LDS
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+#endif
                 if (h) {
 #pragma unroll
                     for (int r = 0; r < TB; ++r) L.li[r * PS + c] = -a[r];    // -X[r][c]
@@ -475,7 +518,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
 size_t gp_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * (size_t)nt * TB;
-    b += sizeof(float) * ((size_t)(nt - 1) * TILE + TB * PS + 2 * (size_t)nt * TB + TB) + 16;
+    b += sizeof(float) * ((size_t)(nt - 1) * TILE + TB * RS + 2 * (size_t)nt * TB + TB) + 16;
     b += sizeof(double) * 3 * nw;
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
     b += sizeof(short) * (size_t)nt * nt;

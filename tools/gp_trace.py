@@ -36,6 +36,9 @@ def main():
         print(f"k={k:2d} start {int(buf[0, k, 0] - t0):8d}  " + " | ".join(row))
     print("totals over waves:", dict(zip(names, tot.tolist())))
     print("walker cycles:", int(buf[:nw, 15, 3].max() - t0))
+    for w in range(nw):
+        hw = int(buf[w, 31, 7])
+        print(f"wave {w}: HW_ID 0x{hw:08x} wave_id {hw & 15} simd {(hw >> 4) & 3} cu {(hw >> 8) & 15} se {(hw >> 13) & 7}")
 
 
 if __name__ == "__main__":
