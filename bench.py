@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
     ap.add_argument("--streams", type=int, default=1, help="independent streams per graph")
     ap.add_argument("--no-gp", action="store_true", help="skip the config-5 GP likelihood measurement")
+    ap.add_argument("--no-predictive", action="store_true", help="skip the posterior-predictive measurement")
     return ap.parse_args()
 
 
@@ -180,6 +181,42 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
             "n_masked_walkers": int((~np.isfinite(out.cpu().numpy())).sum()),
             "cpu_baseline": {"value": 1.0 / cpu_s, "unit": "walker evals/s", "cores": 1, "kind": "port",
                              "sample": f"{k} walkers, fp64 restatement (oracle/gp_oracle.py, scipy LAPACK, 1 thread)"}}
+
+
+def predictive_line(eng, theta, S: int = 100_000, T: int = 1000, reps: int = 5) -> dict:
+    """Posterior predictive (fit.py:2690-2824): total RV (planets + trend) of
+    S posterior samples at T times, one rvk_predict_device launch over the dense [S, T] fp64
+    grid (samples resampled from the config-2 walker block, times spanning the data), HIP events
+    around `reps` launches.  Roofline: the [S, T] fp64 output written to HBM (8 B per solve);
+    the Kepler solves are the same fp64-VALU work as the likelihood's."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rng = np.random.default_rng(7)
+    good = theta[np.all(np.isfinite(theta), axis=1)]
+    samples = good[rng.integers(0, len(good), S)]
+    samples = samples[(samples[:, 2] >= 0) & (samples[:, 2] < 1) & (samples[:, 1] > 0)]   # valid planets only
+    S = len(samples)
+    th = torch.from_numpy(np.ascontiguousarray(samples)).to(dev)
+    tq = torch.linspace(0.0, 1000.0, T, dtype=torch.float64, device=dev)
+    out = torch.empty((S, T), dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    eng.predict_device(th, tq, out, stream=st)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
+        eng.predict_device(th, tq, out, stream=st)
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    ms = a.elapsed_time(b) / reps
+    nbytes = S * T * 8 + S * th.shape[1] * 8 + T * 8
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    ok = bool(torch.isfinite(out).all().item())
+    del out
+    return {"what": f"posterior predictive, {S} samples x {T} times, 1 planet + trend, fp64 [S, T] output in HBM",
+            "ms_per_call": ms, "kepler_solves_per_s": S * T / (ms * 1e-3), "all_finite": ok,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS,
+                         "note": "bytes = 8*S*T output + 8*S*P_full samples + 8*T times per launch / launch time"}}
 
 
 def main():
@@ -360,6 +397,8 @@ def main():
             line["sampler"] = sampler_line(W)
         if world == 1 and not args.no_gp:
             line["gp_config5"] = gp_line()
+        if world == 1 and not args.no_predictive:
+            line["predictive"] = predictive_line(eng, theta)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
         print(json.dumps(line), flush=True)
