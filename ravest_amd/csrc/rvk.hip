@@ -57,6 +57,22 @@ __device__ __forceinline__ void load_tab(SC *lds, const SC *__restrict__ g) {
     __syncthreads();
 }
 
+#ifndef RVK_LL_TRACE
+#define RVK_LL_TRACE 0    // timing experiments only: s_memtime per phase for 4 sampled blocks
+#endif
+#if RVK_LL_TRACE
+__device__ unsigned long long g_ll_trace[16][8];
+#define LL_MARK(slot)                                                                                   \
+    do {                                                                                                \
+        const int tb_ = (blockIdx.x == 0) ? 0 : (blockIdx.x == 100) ? 1 : (blockIdx.x == 500) ? 2 :      \
+                        (blockIdx.x == 1000) ? 3 : -1;                                                  \
+        if (tb_ >= 0 && (threadIdx.x & 63) == 0) g_ll_trace[tb_ * 4 + (threadIdx.x >> 6)][slot] =        \
+            (slot == 0 || slot == 7) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define LL_MARK(slot) do {} while (0)
+#endif
+
 // Block-level structure.  A block (4 waves) owns passes of up to WB walkers
 // (contiguous).  Each pass:
 //   1. prep, lane-parallel over (walker, planet): thread k builds PlanetK for
@@ -102,6 +118,8 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
 #endif
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LL_MARK(0);
+    LL_MARK(1);
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
         // prep (the table fill above lands under the same barrier)
@@ -115,7 +133,9 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             pks[j][p] = pk;
             okp[j][p] = ok;
         }
+        LL_MARK(2);
         __syncthreads();
+        LL_MARK(3);
         for (int j = wv; j < nb; j += kWavesPerBlock) {
             const long long w = base + j;
             const double *row = theta + w * stride;
@@ -199,11 +219,13 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             };
             if ((gd != 0.0) | (gdd != 0.0)) epochs(std::true_type{});
             else epochs(std::false_type{});
+            LL_MARK(4);
             // prod is a frexp mantissa in [0.5, 1) unless the product hit 0 (some s^2 = 0), inf or NaN,
             // whose log is -inf, inf, NaN whatever the exponent
             double lsum = log_frexp(prod, expo);
             if (!(prod >= 0.5 && prod < 1.0)) lsum = prod == 0.0 ? -INFINITY : prod;
             double tot = wave_sum(chi2 + lsum);
+            LL_MARK(5);
             res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
             if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
             }
@@ -232,10 +254,12 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                 }
             } else {
                 if (lane == 0) out[w] = res;
+                LL_MARK(6);
             }
         }
         if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // LDS rows are rewritten next pass
     }
+    LL_MARK(7);
 }
 
 // Segmented variant: LPW lanes per walker, SEG = 64 / LPW walkers per wave (production
@@ -574,6 +598,12 @@ int rvk::fail(int code, const std::string &msg) {
 
 
 extern "C" {
+
+#if RVK_LL_TRACE
+int rvk_ll_trace_dump(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ll_trace), sizeof(g_ll_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int rvk_version(void) { return 100; }
 
