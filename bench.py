@@ -76,10 +76,24 @@ def cpu_baseline(ds, theta, budget_s):
                        ds.parameterisation.code, ds.t0, one, nthreads=1)
         r1 += 1
     el1 = time.perf_counter() - t1
+    # vectorised NumPy leg (the reference arithmetic over a whole walker block
+    # with NumPy arrays, one thread -- what a ravest user gets without numba), ~1/4 of the budget
+    from threadpoolctl import threadpool_limits
+    from oracle import np_oracle
+    blk = sample[:512]
+    r2, t2 = 0, time.perf_counter()
+    with threadpool_limits(1):
+        while time.perf_counter() - t2 < budget_s / 4:
+            np_oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), n_pl, ds.t0, blk)
+            r2 += 1
+    el2 = time.perf_counter() - t2
     return {"value": solves / el, "unit": "Kepler solves/s", "cores": used, "kind": "port",
             "sample": f"{reps} x {len(sample)} walkers x {n_ep} epochs x {n_pl} planet(s) of the same "
                       f"config-{ds.cfg} ensemble, C oracle (oracle/rv_oracle.c, fp64, OpenMP), {el:.1f} s",
-            "single_core_value": r1 * len(one) * n_ep * n_pl / el1}
+            "single_core_value": r1 * len(one) * n_ep * n_pl / el1,
+            "numpy_vectorised_value": r2 * len(blk) * n_ep * n_pl / el2,
+            "numpy_sample": f"{r2} x {len(blk)} walkers, oracle/np_oracle.py (NumPy over [W, N] arrays, 1 thread), "
+                            f"{el2:.1f} s"}
 
 
 def agreement(ds, theta, ll, world, k: int = 512) -> dict:

@@ -75,3 +75,31 @@ def test_loglike_vs_reference(name):
                            len(m["planet_letters"]), PARAMETERISATION_CODE[m["parameterisation"]], m["t0"],
                            case["theta_full"])
     assert_ll_close(ll, case["log_like"], rtol=ORACLE_RTOL, what=name)
+
+
+def test_numpy_restatement_matches_c_oracle():
+    """oracle/np_oracle.py (vectorised NumPy restatement, the CPU baseline's NumPy leg) equals the
+    pinned C oracle on config-2/3 shaped blocks incl. invalid and circular walkers."""
+    from oracle import np_oracle
+    from ravest_amd.synth import CONFIGS, make_dataset, make_walkers
+    for cfg in (2, 3):
+        c = CONFIGS[cfg]
+        ds = make_dataset(c["n_planets"], min(c["n_epochs"], 256), c["n_inst"], seed=c["seed"])
+        th = make_walkers(ds, 128, seed=c["seed"])
+        th[:8, 2] = 0.0                                   # circular orbits (model.py:236-241)
+        ni, npl = len(ds.unique_instruments), len(ds.planet_letters)
+        ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, npl, ds.parameterisation.code,
+                                ds.t0, th)
+        got = np_oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, npl, ds.t0, th)
+        fin = np.isfinite(ref)
+        assert np.array_equal(np.isfinite(got), fin)
+        assert (~fin).sum() > 0
+        np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-13, atol=0)
+
+
+def test_numpy_kepler_matches_golden_grid():
+    """The vectorised Halley solver against the reference's own Kepler outputs (golden grid)."""
+    from oracle import np_oracle
+    g = np.load(f"{GOLDEN}/kepler_grid.npz")
+    c, s = np_oracle.solve_kepler(g["M"], g["e"])
+    assert np.max(np.abs(c - g["cosE"])) <= 1e-16 and np.max(np.abs(s - g["sinE"])) <= 1e-16
