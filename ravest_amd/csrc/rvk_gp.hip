@@ -87,7 +87,8 @@ __device__ __forceinline__ int cd_row(int r, int lane) { return (r & 3) + 8 * (r
 
 struct GpLds {
     // carved from dynamic shared memory
-    double *t;       // [npad]          epoch times (padding: copies of t[n-1])
+    float *uph;      // [npad]          per walker: fract(t_i / P_gp) (fp64 reduction, then fp32)
+    float *tsc;      // [npad]          per walker: (t_i - t_0) / lambda_e (padding: t[n-1]'s)
     float *pan;      // [nt - 1][TILE]  tile rows 1.. of the column in flight (C/D register order);
                      //                 after S1(k) slot k holds L(k+1, k), read by every wave in S2(k)
     float *li;       // [TB][RS]        inverse of the step's diagonal tile, row-major (stride PS);
@@ -105,8 +106,11 @@ struct GpLds {
 template <int NW>
 __device__ __forceinline__ GpLds carve(void *smem, int nt) {
     GpLds L;
-    L.t = reinterpret_cast<double *>(smem);
-    float *f = reinterpret_cast<float *>(L.t + nt * TB);
+    float *f = reinterpret_cast<float *>(smem);
+    L.uph = f;
+    f += nt * TB;
+    L.tsc = f;
+    f += nt * TB;
     L.pan = f;
     f += (nt - 1) * TILE;
     L.li = f;
@@ -159,7 +163,6 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
     }
 #endif
     for (int i = tid; i < kTabN; i += NT) L.tab[i] = d.tab[i];
-    for (int i = tid; i < nt * TB; i += NT) L.t[i] = d.t[i < n ? i : n - 1];
     for (int i = tid; i < nt * nt; i += NT) L.slot[i] = slots[i];
     float *A = work + (long long)blockIdx.x * work_stride;
 
@@ -184,7 +187,15 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
         }
         const double *g = row + 5 * np, *jit = g + ni;
         const double gd = jit[ni], gdd = jit[ni + 1];
+        const double amp = hp[0], lam_e = hp[1], lam_p = hp[2], per = hp[3];
+        const double inv_per = 1.0 / per, inv_le = 1.0 / lam_e, tref = d.t[0];
         for (int i = tid; i < npad; i += NT) {
+            // covariance inputs: sin^2(pi (t_i - t_j) / P) needs only the phase fractions (their
+            // difference is exact to fp32 rounding), exp(-(t_i - t_j)^2 / 2 lambda_e^2) the scaled
+            // times relative to t_0 (bounded by the span of the data, not by BJD magnitudes)
+            const double ti = d.t[i < n ? i : n - 1];
+            L.uph[i] = (float)__builtin_amdgcn_fract(ti * inv_per);
+            L.tsc[i] = (float)((ti - tref) * inv_le);
             float ri = 0.0f, di = 1.0f;
             if (i < n) {
                 const double t = d.t[i];
@@ -202,28 +213,22 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
         }
         __syncthreads();
         // ---- 2. pipelined blocked Cholesky ---------------------------------------------------
-        const double amp = hp[0], lam_e = hp[1], lam_p = hp[2], per = hp[3];
         const float namp2 = -(float)(amp * amp);
         const float gam = (float)(1.0 / (2.0 * lam_p * lam_p));   // gp.py:150
-        const double inv_per = 1.0 / per;
         // -C(bi, bj)^T in C/D layout: lane l, register r = -C[bi*32 + (l & 31)][bj*32 + cd_row(r, l)]
         // (gp.py:126-156 + fit.py:8090-8105); padding rows/columns are identity.  Accumulators hold
         // the NEGATED trailing tiles, -acc = -C + sum L L^T, so every MFMA adds (no sign flips).
-        const float inv_le = (float)(1.0 / lam_e);
         auto cov_tile = [&](int bi, int bj, f32x16 &t) {
-            const double ti = L.t[bi * TB + c];
+            const float ui = L.uph[bi * TB + c], si = L.tsc[bi * TB + c];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const double2 p0 = *reinterpret_cast<const double2 *>(L.t + bj * TB + 8 * u + 4 * h);
-                const double2 p1 = *reinterpret_cast<const double2 *>(L.t + bj * TB + 8 * u + 4 * h + 2);
-                const double tj[4] = {p0.x, p0.y, p1.x, p1.y};
+                const float4 uj = *reinterpret_cast<const float4 *>(L.uph + bj * TB + 8 * u + 4 * h);
+                const float4 sj = *reinterpret_cast<const float4 *>(L.tsc + bj * TB + 8 * u + 4 * h);
+                const float ujv[4] = {uj.x, uj.y, uj.z, uj.w}, sjv[4] = {sj.x, sj.y, sj.z, sj.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const double tau = ti - tj[e];
-                    // sin^2(pi tau / P): the phase's fraction in fp64, then v_sin_f32 (revolutions)
-                    const float fr = (float)__builtin_amdgcn_fract(tau * inv_per);
-                    const float sn = __builtin_amdgcn_sinf(0.5f * fr);
-                    const float x = (float)tau * inv_le;
+                    const float sn = __builtin_amdgcn_sinf(0.5f * (ui - ujv[e]));   // v_sin_f32: revolutions
+                    const float x = si - sjv[e];
                     t[4 * u + e] = namp2 * __expf(-(gam * (sn * sn) + 0.5f * (x * x)));
                 }
             }
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
 
 size_t gp_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
-    size_t b = sizeof(double) * (size_t)nt * TB;
+    size_t b = sizeof(float) * 2 * (size_t)nt * TB;
     b += sizeof(float) * ((size_t)(nt - 1) * TILE + TB * RS + 2 * (size_t)nt * TB + TB) + 16;
     b += sizeof(double) * 3 * nw;
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;

@@ -53,6 +53,22 @@ def test_gp_loglike_vs_fp64_oracle(n, np_, ni, par, trend):
     assert np.isfinite(ref).sum() >= 40
 
 
+def test_gp_bjd_times():
+    """BJD-scale epochs (t ~ 2.46e6 d): the covariance's phase fractions and scaled times are
+    formed in fp64 relative to the data, so fp32 keeps its precision."""
+    from oracle import gp_oracle
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(1, 200, 1, seed=77, t_offset=2457000.25)
+    rng = np.random.default_rng(77)
+    th = make_walkers(ds, 32, seed=77, scale=0.002)
+    th[:, 6] = np.abs(th[:, 6])
+    hy = np.column_stack([rng.uniform(2, 6, 32), rng.uniform(30, 120, 32), rng.uniform(0.3, 1.0, 32),
+                          rng.uniform(10, 40, 32)])
+    ll = _gp(ds).batch(th, hy)
+    ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th, hy)
+    _check(ll, ref, "bjd")
+
+
 def test_gp_config5_shape_and_paths():
     """Config-5 shape (1 planet + GP, 512 epochs): host path == device path, repeatable,
     invalid planets -inf, and parity with the fp64 oracle on a sample of walkers."""
