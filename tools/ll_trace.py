@@ -13,14 +13,22 @@ def main():
     from ravest_amd.synth import CONFIGS, make_dataset, make_walkers
     c = CONFIGS[2]
     ds = make_dataset(c["n_planets"], c["n_epochs"], c["n_inst"], seed=c["seed"])
-    th = make_walkers(ds, 4096, seed=c["seed"])
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    th = make_walkers(ds, W, seed=c["seed"])
     eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, ds.parameterisation, ds.t0, device=0)
-    eng.reserve(4096)
+    eng.reserve(W)
     t = torch.from_numpy(th).cuda()
-    out = torch.empty(4096, dtype=torch.float64, device="cuda")
+    out = torch.empty(W, dtype=torch.float64, device="cuda")
     for _ in range(50):
         eng.loglike_device(t, out)
     torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(50):
+        eng.loglike_device(t, out)
+    b.record()
+    torch.cuda.synchronize()
+    print(f"W={W}: {a.elapsed_time(b) / 50 * 1e3:.2f} us per launch (eager, incl. launch gaps)")
     buf = np.zeros((16, 8), dtype=np.uint64)
     assert _lib.load().rvk_ll_trace_dump(buf.ctypes.data_as(C.c_void_p)) == 0
     r0 = buf[:, 0].astype(np.int64).min()
