@@ -14,7 +14,8 @@
 //  * solve_kepler_fast -- the production solver (default).  It converges to
 //    the same root to ~1 ulp, so cos E / sin E match the reference's converged
 //    values within the stated fp64 tolerance:
-//      1. r = M reduced to [-pi, pi] (Cody-Waite, FMA);
+//      1. r = M reduced to [-pi, pi] (Cody-Waite, FMA); planet_rv instead reduces the
+//         phase u = (t - Tp) / P exactly, r = 2 pi (u - rint u);
 //      2. fp32 Halley seed from E0 = r with the hardware v_sin_f32/v_cos_f32
 //         (accurate fp32 polynomials when e > 0.95, wave-uniform branch),
 //         started from the series E0 = r + e sin r (1 + e cos r); per-lane exit
@@ -220,10 +221,9 @@ __device__ __forceinline__ float seed_f32(float rf, float ef) {
     return Ef;
 }
 
-// e6e3 = 6*e^3 (per planet, precomputed).
-__device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e3, const SC *tab, double &cosE,
-                                                  double &sinE) {
-    const double r = reduce_2pi(M);
+// r = the mean anomaly reduced to [-pi, pi]; e6e3 = 6*e^3 (per planet, precomputed).
+__device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e6e3, const SC *tab, double &cosE,
+                                                    double &sinE) {
     const float rf = (float)r, ef = (float)e;
 #ifndef RVK_SEED_HW
 #define RVK_SEED_HW 1
@@ -238,16 +238,27 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
 #ifndef RVK_HH_SINGLE
 #define RVK_HH_SINGLE 1
 #endif
-    // One Householder (order 3) step from (E, S = sin E, C = cos E); returns the step d
-    // and leaves t ~ 1/den for the error estimate.
-    auto step = [&](double &t) -> double {
+#ifndef RVK_HALLEY_LOWE
+#define RVK_HALLEY_LOWE 0   // 1: e <= 0.5 takes a Halley first fp64 step (cubic, 6 fewer fp64 ops);
+                            // measured a wash (-1.6 % .. +4 % over the kbench cases), so off
+#endif
+    // One step from (E, S = sin E, C = cos E), Halley's (hal) or Householder's of order 3;
+    // returns the step d and leaves t ~ 1/den for the error estimate.  Only num/den sit under
+    // the branch, so a wave whose lanes disagree on hal runs the shared rest once.
+    auto step = [&](bool hal, double &t) -> double {
         const double f = E - e * S - r;
         const double f1 = 1.0 - e * C;
         const double f2 = e * S;
-        const double f3 = e * C;
-        const double f11 = f1 * f1;
-        const double num = f * __builtin_fma(-3.0 * f, f2, 6.0 * f11);                        // f (6 f1^2 - 3 f f2)
-        const double den = __builtin_fma(f * f, f3, 6.0 * f1 * __builtin_fma(-f, f2, f11));  // 6f1^3 - 6 f f1 f2 + f^2 f3
+        double num, den;
+        if (hal) {
+            num = f * f1;                                                            // f f1 / (f1^2 - f f2 / 2)
+            den = __builtin_fma(-0.5 * f, f2, f1 * f1);
+        } else {
+            const double f3 = e * C;
+            const double f11 = f1 * f1;
+            num = f * __builtin_fma(-3.0 * f, f2, 6.0 * f11);                        // f (6 f1^2 - 3 f f2)
+            den = __builtin_fma(f * f, f3, 6.0 * f1 * __builtin_fma(-f, f2, f11));  // 6f1^3 - 6 f f1 f2 + f^2 f3
+        }
         t = __builtin_amdgcn_rcp(den);
         t = __builtin_fma(t, __builtin_fma(-den, t, 1.0), t);
         const double d = -num * t;
@@ -272,18 +283,27 @@ __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e
         const double z2 = (d * d) * (d * d);
         return z2 * e6e3 * __builtin_fabs(t) < 1e-17;
     };
-    // the first step is peeled (no loop-carried register shuffles on the common one-step path)
+    // The first step is peeled (no loop-carried register shuffles on the common one-step path).
+    // Halley's next error is c d^3 with |c| = |f2^2 / (4 f1^2) - f3 / (6 f1)| <= 0.42 for
+    // e <= 0.5 (f1 >= 1/2, |f2|, |f3| <= 1/2): |d| <= 2.8e-6 bounds it by 9.2e-18.
+    const bool hal = RVK_HALLEY_LOWE && e <= 0.5;
     double t;
-    double d = step(t);
-    if (!converged(d, t)) {
+    double d = step(hal, t);
+    const bool done = hal ? __builtin_fabs(d) <= 2.8e-6 : converged(d, t);
+    if (!done) {
 #pragma unroll 1
         for (int it = 1; it < 8; ++it) {
-            d = step(t);
+            d = step(false, t);
             if (converged(d, t)) break;
         }
     }
     cosE = C;
     sinE = S;
+}
+
+__device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e3, const SC *tab, double &cosE,
+                                                  double &sinE) {
+    solve_kepler_fast_r(reduce_2pi(M), e, e6e3, tab, cosE, sinE);
 }
 
 // ---- register-light atan / atan2 / tan for the Tc and secosw/sesinw conversions ----
@@ -345,8 +365,11 @@ __device__ __forceinline__ double tan_fd(double x) {
 // rv = K * (inv * ((cosE - e) * cw - sinE * sqsw) + ecw),  inv = 1 / (1 - e cosE)
 // (= K (cos f cos w - sin f sin w + e cos w), model.py:119-121,170; K stays the
 // outer factor so K = inf gives +-inf like the reference, not inf - inf)
+#ifndef RVK_PHASE
+#define RVK_PHASE 1   // planet_rv reduces the phase (t - Tp) / P rather than M = n (t - Tp)
+#endif
 struct PlanetK {
-    double n, Tp, e, K, cw, sqsw, ecw, e6e3;
+    double n, Tp, e, K, cw, sqsw, ecw, e6e3;   // n = 1 / P (RVK_PHASE) or 2 pi / P
 };
 
 // param.py:88-105 (NaN passes the '<=' tests, as in the reference)
@@ -405,7 +428,7 @@ __device__ __forceinline__ bool planet_consts_t(const double *p5, PlanetK &pk, i
     if (!ok) {                            // keep the masked walker's arithmetic finite
         P = 1.0; e = 0.0; w = 0.0;
     }
-    pk.n = kTwoPi / P;
+    pk.n = RVK_PHASE ? 1.0 / P : kTwoPi / P;
     pk.Tp = Tp;
     pk.e = e;
     double sw, cw;
@@ -431,10 +454,21 @@ template <int SOLVER>
 // acc + (this planet's RV at t).  1/(1 - e cos E) with one Newton step on v_rcp_f64
 // (<= 2.2e-15 relative, like the chi^2 terms); the divisor is in (0, 2).
 __device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const SC *tab, double acc) {
-    const double M = pk.n * (t - pk.Tp);
     double cE, sE;
-    if (SOLVER == 1) solve_kepler_ref(M, pk.e, cE, sE);
-    else solve_kepler_fast(M, pk.e, pk.e6e3, tab, cE, sE);
+    if (SOLVER == 1) {
+        const double M = RVK_PHASE ? kTwoPi * (pk.n * (t - pk.Tp)) : pk.n * (t - pk.Tp);
+        solve_kepler_ref(M, pk.e, cE, sE);
+    } else if (RVK_PHASE) {
+        // orbits since periastron u = (t - Tp) / P: u - rint(u) is exact, so r = 2 pi (u - rint u)
+        // is M reduced to [-pi, pi] to |M| 2.2e-16 + ulp(pi) (|u| >= 2^52: r = 0), in 5 VALU
+        // instructions instead of M and a Cody-Waite reduction's 12.  Not contracted: fusing the
+        // product into the subtraction would leave its rounding error, ~ulp(u), in the fraction.
+#pragma clang fp contract(off)
+        const double u = pk.n * (t - pk.Tp);
+        solve_kepler_fast_r(kTwoPi * (u - __builtin_rint(u)), pk.e, pk.e6e3, tab, cE, sE);
+    } else {
+        solve_kepler_fast(pk.n * (t - pk.Tp), pk.e, pk.e6e3, tab, cE, sE);
+    }
     const double b = 1.0 - pk.e * cE;
     double inv = __builtin_amdgcn_rcp(b);
     inv = __builtin_fma(inv, __builtin_fma(-b, inv, 1.0), inv);
