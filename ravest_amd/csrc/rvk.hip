@@ -46,9 +46,20 @@ namespace {
 #ifndef RVK_TP_INLINE
 #define RVK_TP_INLINE 1               // "P K e w Tp": inline conversion in the prep (1) or the out-of-line one (0)
 #endif
+#ifndef RVK_EPOCH_OFF32
+#define RVK_EPOCH_OFF32 1             // epoch loads through one 32-bit byte offset (global_load saddr form)
+#endif
 #ifndef RVK_LB_WAVES
 #define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
+
+// base[off / sizeof(T)] for a byte offset below 4 GiB: the 64-bit base stays in SGPRs and the
+// 32-bit offset is the load's VGPR operand (global_load's saddr form), so a lane advancing
+// through the epochs keeps one 32-bit induction variable instead of a 64-bit address per array.
+template <class T>
+__device__ __forceinline__ T ld_off(const T *base, unsigned off) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
+}
 
 // Copy the sin/cos table into LDS (whole block; one barrier, before any
 // per-wave work so no wave can skip it).
@@ -166,7 +177,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                             if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
                         }
                     }
-                    double rv = gam;   // each planet's K * (...) lands in one FMA
+                    double rv = gam - vel;   // the residual itself: each planet's K * (...) lands in one FMA
 #pragma unroll
                     for (int p = 0; p < NP; ++p) rv = planet_rv<SOLVER>(pk[p], t, tab, rv);
                     if (TREND) {
@@ -174,7 +185,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                         rv += __builtin_fma(gd, dt, gdd * (dt * dt));
                     }
                     const double s2 = s2b + jj;
-                    const double r = rv - vel;
+                    const double r = rv;
 #if RVK_CHI_NR2
                     chi2 = __builtin_fma(r * r, rcp_nr(s2), chi2);
 #else
@@ -202,6 +213,22 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
                     one(tB, vB, sB, iB);
                 }
                 if (i < n_epochs) one(tA, vA, sA, iA);
+#elif RVK_EPOCH_OFF32
+                // one epoch per trip; the next epoch's loads are issued before this one's solve.
+                // off = 8 (i + 64), the next epoch's byte offset, is the only induction variable:
+                // epoch i is live while off < 8 n + 512, epoch i + 64 exists while off < 8 n.
+                double tn = t_1, vn = v_1, sn = s_1;
+                int in_ = i_1;
+                const unsigned lim = 8u * (unsigned)n_epochs;
+                for (unsigned off = 8u * (unsigned)(lane + 64); off < lim + 512u; off += 512u) {
+                    const double t = tn, vel = vn, s2b = sn;
+                    const int ii = in_;
+                    if (off < lim) {
+                        tn = ld_off(d.t, off); vn = ld_off(d.vel, off); sn = ld_off(d.s2, off);
+                        if (MULTI) in_ = ld_off(d.inst, off >> 1);
+                    }
+                    one(t, vel, s2b, ii);
+                }
 #else
                 // one epoch per trip; the next epoch's loads are issued before this one's solve
                 double tn = t_1, vn = v_1, sn = s_1;
@@ -321,6 +348,17 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
                 constexpr bool TREND = decltype(trend_c)::value;
                 double tn = t_1, vn = v_1, sn = s_1;
                 int in_ = i_1;
+#if RVK_EPOCH_OFF32
+                // off = 8 (i + LPW): the only induction variable (as in loglike_kernel)
+                const unsigned lim = 8u * (unsigned)n_epochs;
+                for (unsigned off = 8u * (unsigned)(li + LPW); off < lim + 8u * LPW; off += 8u * LPW) {
+                    const double t = tn, vel = vn, s2b = sn;
+                    const int ii = in_;
+                    if (off < lim) {
+                        tn = ld_off(d.t, off); vn = ld_off(d.vel, off); sn = ld_off(d.s2, off);
+                        if (MULTI) in_ = ld_off(d.inst, off >> 1);
+                    }
+#else
                 for (int i = li; i < n_epochs; i += LPW) {
                     const double t = tn, vel = vn, s2b = sn;
                     const int ii = in_;
@@ -328,13 +366,14 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
                         tn = d.t[i + LPW]; vn = d.vel[i + LPW]; sn = d.s2[i + LPW];
                         if (MULTI) in_ = d.inst[i + LPW];
                     }
+#endif
                     double gam = g0, jj = j0sq;
                     if (MULTI) {
                         for (int k = 1; k < n_inst; ++k) {
                             if (ii == k) { gam = g[k]; jj = jit[k] * jit[k]; }
                         }
                     }
-                    double rv = gam;
+                    double rv = gam - vel;   // the residual itself (as in loglike_kernel)
 #pragma unroll
                     for (int p = 0; p < NP; ++p) rv = planet_rv<0>(pk[p], t, tab, rv);
                     if (TREND) {
@@ -342,7 +381,7 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
                         rv += __builtin_fma(gd, dt, gdd * (dt * dt));
                     }
                     const double s2 = s2b + jj;
-                    const double r = rv - vel;
+                    const double r = rv;
                     chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);
                     prod *= s2;
                     int ex;

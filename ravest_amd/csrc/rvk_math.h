@@ -168,11 +168,16 @@ __device__ __forceinline__ double fma_s(double a, double b, double c) {
 }
 
 __device__ __forceinline__ void sincos_tab(double E, const SC *tab, double &S, double &C) {
-    double jj = __builtin_rint(E * kTabInvH);
-    jj = __builtin_fmin(__builtin_fmax(jj, (double)-kTabHalf), (double)kTabHalf);
+    const double jj = __builtin_rint(E * kTabInvH);
     const double a = jj * kTabH;                 // same rounding as the host's j*h
     const double d = E - a;                      // exact (Sterbenz)
-    const SC sc = tab[(int)jj + kTabHalf];
+    // only the index is clamped (one v_med3_i32): |E| <= pi + 1e-6 for every finite solve;
+    // a NaN/inf E gives a NaN d, a garbage one a garbage value, never an out-of-table read.
+    // v_cvt_i32_f64 itself saturates and maps NaN to 0 (asm: no C++ out-of-range conversion).
+    int ji;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(ji) : "v"(jj));
+    ji = ji < -kTabHalf ? -kTabHalf : (ji > kTabHalf ? kTabHalf : ji);
+    const SC sc = tab[ji + kTabHalf];
     const double z = d * d;
     const double sd = __builtin_fma(d * z, fma_s(z, fma_s(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), d);
     const double cm = z * __builtin_fma(z, fma_s(z, fma_s(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
