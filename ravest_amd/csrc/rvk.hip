@@ -49,6 +49,11 @@ namespace {
 #ifndef RVK_EPOCH_OFF32
 #define RVK_EPOCH_OFF32 1             // epoch loads through one 32-bit byte offset (global_load saddr form)
 #endif
+#ifndef RVK_PK_SGPR
+#define RVK_PK_SGPR 2                 // NP >= this: planet constants moved to SGPRs, else left in VGPRs
+                                      // (NP = 1 in VGPRs: 34 -> 7 SGPR spills, -2.5 % config 2;
+                                      //  NP = 3 in VGPRs: +3.6 %)
+#endif
 #ifndef RVK_LB_WAVES
 #define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
             const double g0 = g[0], j0 = jit[0] * jit[0];
             PlanetK pk[NP];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) pk[p] = uniform_pk(pks[j][p]);
+            for (int p = 0; p < NP; ++p) pk[p] = NP >= RVK_PK_SGPR ? uniform_pk(pks[j][p]) : pks[j][p];
             double chi2 = 0.0, prod = 0.5;   // prod * 2^expo = running product of s^2
             int expo = 1;
             // The epoch loop, versioned on the (wave-uniform) trend so the trend-free
