@@ -16,7 +16,8 @@
 //    values within the stated fp64 tolerance:
 //      1. r = M reduced to [-pi, pi] (Cody-Waite, FMA); planet_rv instead reduces the
 //         phase u = (t - Tp) / P exactly, r = 2 pi (u - rint u);
-//      2. fp32 Halley seed from E0 = r with the hardware v_sin_f32/v_cos_f32
+//      2. e <= 0.18: the e^4 Lagrange series (seed_series), else
+//         fp32 Halley seed from E0 = r with the hardware v_sin_f32/v_cos_f32
 //         (accurate fp32 polynomials when e > 0.95, wave-uniform branch),
 //         started from the series E0 = r + e sin r (1 + e cos r); per-lane exit
 //         once an update is < 1e-2 (Halley is cubic: the error after it is
@@ -226,6 +227,25 @@ __device__ __forceinline__ float seed_f32(float rf, float ef) {
     return Ef;
 }
 
+#ifndef RVK_SERIES_E
+#define RVK_SERIES_E 0.18f    // e <= this: the seed is the e^4 Lagrange series, no fp32 Halley step
+#endif
+// E = r + s [e + e^2 c + e^3 (1 - 3/2 s^2) + e^4 c (1 - 8/3 s^2)] + O(e^5), s, c = sin r, cos r
+// (Lagrange's inversion of Kepler's equation to 4th order).  The e^5 remainder is at most
+// 0.54 e^5: <= 1.0e-4 for e <= 0.18 (2.5e-5 at e = 0.136), so one Householder step ends the
+// solve (error <= (e/f')^3 d^4 <= 0.0106 d^4 < 1e-17 for |d| <= 1.7e-4) at the cost of two
+// v_sin/v_cos and ~10 fp32 ops instead of the starter plus a Halley iteration.
+__device__ __forceinline__ float seed_series(float rf, float ef) {
+    float s, c;
+    sincos_seed<false>(rf, s, c);
+    const float s2 = s * s;
+    const float a4 = c * __builtin_fmaf(-2.66666667f, s2, 1.0f);
+    float q = __builtin_fmaf(ef, a4, __builtin_fmaf(-1.5f, s2, 1.0f));
+    q = __builtin_fmaf(ef, q, c);
+    q = __builtin_fmaf(ef, q, 1.0f);
+    return __builtin_fmaf(s, ef * q, rf);
+}
+
 // r = the mean anomaly reduced to [-pi, pi]; e6e3 = 6*e^3 (per planet, precomputed).
 __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e6e3, const SC *tab, double &cosE,
                                                     double &sinE) {
@@ -236,7 +256,10 @@ __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e
 #ifndef RVK_ABLATE
 #define RVK_ABLATE 0   // timing experiments only (wrong results): 1 = no fp64 stage, 2 = no fp32 seed, 3 = neither
 #endif
-    const float Ef = (RVK_ABLATE & 2) ? rf : ((!RVK_SEED_HW || ef > 0.95f) ? seed_f32<true>(rf, ef) : seed_f32<false>(rf, ef));
+    const bool series = ef <= RVK_SERIES_E;
+    const float Ef = (RVK_ABLATE & 2) ? rf
+                   : series ? seed_series(rf, ef)
+                   : ((!RVK_SEED_HW || ef > 0.95f) ? seed_f32<true>(rf, ef) : seed_f32<false>(rf, ef));
     double E = (double)Ef, S, C;
     sincos_tab(E, tab, S, C);
     if (RVK_ABLATE & 1) { cosE = C; sinE = S; return; }
@@ -294,7 +317,7 @@ __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e
     const bool hal = RVK_HALLEY_LOWE && e <= 0.5;
     double t;
     double d = step(hal, t);
-    const bool done = hal ? __builtin_fabs(d) <= 2.8e-6 : converged(d, t);
+    const bool done = hal ? __builtin_fabs(d) <= 2.8e-6 : series ? __builtin_fabs(d) <= 1.7e-4 : converged(d, t);
     if (!done) {
 #pragma unroll 1
         for (int it = 1; it < 8; ++it) {
