@@ -54,6 +54,10 @@ namespace {
                                       // (NP = 1 in VGPRs: 34 -> 7 SGPR spills, -2.5 % config 2;
                                       //  NP = 3 in VGPRs: +3.6 %)
 #endif
+#ifndef RVK_LL_BLOCK
+#define RVK_LL_BLOCK 1024             // threads per loglike_kernel block for NP = 1 and W >= 256 blocks' worth
+                                      // (one wave preps 16 walkers: -7 % "P K e w Tc", +-0 "P K e w Tp")
+#endif
 #ifndef RVK_LB_WAVES
 #define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
@@ -110,8 +114,8 @@ struct PassCfg {
     static constexpr int WB = (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
 };
 
-template <int NP, bool MULTI, int SOLVER, bool TP, bool SAMPLE>
-__global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
+template <int NP, bool MULTI, int SOLVER, bool TP, bool SAMPLE, int BLK = kBlock>
+__global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
                                                          long long stride, int wb, double *__restrict__ out,
                                                          PostArgs post, SampleArgs sa) {
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
     }
 #if RVK_TAB_LDS
     __shared__ SC tab[kTabN];
-    for (int i = threadIdx.x; i < kTabN; i += kBlock) tab[i] = d.tab[i];
+    for (int i = threadIdx.x; i < kTabN; i += BLK) tab[i] = d.tab[i];
 #else
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
 #endif
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
         // prep (the table fill above lands under the same barrier)
-        for (int k = threadIdx.x; k < nb * NP; k += kBlock) {
+        for (int k = threadIdx.x; k < nb * NP; k += BLK) {
             const int j = k / NP, p = k - j * NP;
             const long long w = base + j;
             const double *p5 = theta + w * stride + 5 * p;
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(kBlock, (NP == 1 ? 4 : RVK_LB_WAVES)) void loglike_
         LL_MARK(2);
         __syncthreads();
         LL_MARK(3);
-        for (int j = wv; j < nb; j += kWavesPerBlock) {
+        for (int j = wv; j < nb; j += BLK / 64) {
             const long long w = base + j;
             const double *row = theta + w * stride;
             const double lpw = post.lp ? post.lp[w] : 0.0;      // log-prior (posterior / sampler mode)
@@ -491,13 +495,13 @@ thread_local std::string g_err;
 constexpr long long kMaxBlocks = 2048;
 
 template <int NP>
-void ll_grid(long long W, long long &blocks, int &wb) {
+void ll_grid(long long W, long long &blocks, int &wb, int wpb = kWavesPerBlock) {
     constexpr int WB = PassCfg<NP>::WB;
-    blocks = (W + kWavesPerBlock - 1) / kWavesPerBlock;
-    wb = kWavesPerBlock;
+    blocks = (W + wpb - 1) / wpb;
+    wb = wpb;
     if (blocks > kMaxBlocks) {
         long long per = (W + kMaxBlocks - 1) / kMaxBlocks;                 // walkers per block
-        per = ((per + kWavesPerBlock - 1) / kWavesPerBlock) * kWavesPerBlock;
+        per = ((per + wpb - 1) / wpb) * wpb;
         wb = (int)(per < WB ? per : WB);
         blocks = (W + wb - 1) / wb;
         if (blocks > kMaxBlocks) blocks = kMaxBlocks;
@@ -541,6 +545,12 @@ void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, lon
     }
     long long blocks;
     int wb;
+    if (NP == 1 && RVK_LL_BLOCK > kBlock && W >= 256LL * (RVK_LL_BLOCK / 64)) {   // >= one block per CU
+        ll_grid<NP>(W, blocks, wb, RVK_LL_BLOCK / 64);
+        hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, false, RVK_LL_BLOCK>), dim3((unsigned)blocks),
+                           dim3(RVK_LL_BLOCK), 0, st, d, n, ni, th, W, stride, wb, out, post, SampleArgs{});
+        return;
+    }
     ll_grid<NP>(W, blocks, wb);
     hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d,
                        n, ni, th, W, stride, wb, out, post, SampleArgs{});
