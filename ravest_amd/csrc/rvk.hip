@@ -160,6 +160,18 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             const long long w = base + j;
             const double *row = theta + w * stride;
             const double lpw = post.lp ? post.lp[w] : 0.0;      // log-prior (posterior / sampler mode)
+            // SAMPLE: the accept test's operands are loaded before the epoch loop, so their latency
+            // (sidx -> lp[sidx] is a dependent pair) hides under the loop instead of the wave's tail
+            long long sw_s = 0;
+            double lp_old_s = 0.0, fac_s = 0.0, au_s = 1.0;
+            if constexpr (SAMPLE) {
+                sw_s = sa.sidx[w];
+                // (a global-address-space load: a flat one would also hold lgkmcnt, which the
+                // epoch loop's LDS reads wait on)
+                lp_old_s = *(const __attribute__((address_space(1))) double *)(sa.run->lp + sw_s);
+                fac_s = sa.fac[w];
+                au_s = sa.au[w];
+            }
             bool all_ok = true;
 #pragma unroll
             for (int p = 0; p < NP; ++p) all_ok &= okp[j][p] != 0;
@@ -268,9 +280,9 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             if constexpr (SAMPLE) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
                 const RunArgs &run = *sa.run;
                 const int D = sa.D;
-                const long long sw = sa.sidx[w];
-                const double lp_old = run.lp[sw];
-                const bool acc = sa.fac[w] + res - lp_old > log(sa.au[w]);
+                const long long sw = sw_s;
+                const double lp_old = lp_old_s;
+                const bool acc = fac_s + res - lp_old > log(au_s);
                 double *xs = run.x + sw * D;
                 const double *qw = sa.q + w * D;
                 const long long W2 = 2 * n_walkers;
