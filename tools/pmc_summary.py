@@ -9,22 +9,31 @@ from collections import defaultdict
 
 out_dir, cfg = sys.argv[1], sys.argv[2]
 kfilter = sys.argv[3] if len(sys.argv) > 3 else None   # kernel-name substring (default: the plain loglike launch)
-vals = defaultdict(float)
-disp = defaultdict(set)
-kname = None
+
+def plain_loglike(name):
+    """loglike_kernel<NP, MULTI, SOLVER, TP, SAMPLE[, BLK]> with SAMPLE = false (not the sampler's)."""
+    if "loglike_kernel<" not in name:
+        return False
+    args = name.split("loglike_kernel<", 1)[1].split(">(", 1)[0].split(", ")
+    return len(args) >= 5 and args[4] == "false"
+
+
+vals = defaultdict(lambda: defaultdict(float))
+disp = defaultdict(lambda: defaultdict(set))
 for f in sorted(glob.glob(os.path.join(out_dir, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for row in csv.DictReader(open(f)):
         name = row.get("Kernel_Name", "")
         if kfilter is not None:
             if kfilter not in name:
                 continue
-        elif "loglike_kernel<" not in name or ", false>(" not in name:   # the plain (non-sampler) launch
+        elif not plain_loglike(name):
             continue
-        kname = name
         c = row["Counter_Name"]
-        vals[c] += float(row["Counter_Value"])
-        disp[c].add(row.get("Dispatch_Id", row.get("Correlation_Id")))
-per = {c: vals[c] / max(1, len(disp[c])) for c in vals}
+        vals[name][c] += float(row["Counter_Value"])
+        disp[name][c].add(row.get("Dispatch_Id", row.get("Correlation_Id")))
+# the measured kernel: the matching instantiation with the most dispatches
+kname = max(disp, key=lambda k: max(len(v) for v in disp[k].values())) if disp else None
+per = {c: vals[kname][c] / max(1, len(disp[kname][c])) for c in vals[kname]} if kname else {}
 src = (f"rocprofv3 --pmc passes over `python tools/gp_bench.py` (tools/pmc_gp.sh)" if kfilter else
        f"rocprofv3 --pmc passes over `python bench.py --config {cfg} --steps 20 --warmup 5 --no-cpu-baseline --no-sampler` (tools/pmc.sh)")
 res = {"kernel": kname, "counters_per_launch": per, "source": src}
