@@ -54,8 +54,8 @@ def test_kepler_random_vs_oracle(eng_mod, solver):
 
 
 def test_kepler_low_eccentricity_vs_oracle(eng_mod):
-    """e <= 0.5 takes a Halley first fp64 step (rvk_math.h); waves that mix e <= 0.5 and e > 0.5
-    lanes run both step forms under the lane mask."""
+    """Low eccentricities: e <= 0.18 takes the e^4-series seed and one Householder step, larger
+    e the fp32 Halley seed (rvk_math.h); waves mixing both run each path under the lane mask."""
     from oracle import oracle
     rng = np.random.default_rng(11)
     M = np.concatenate([rng.uniform(-10, 10, 24000), rng.uniform(-1e4, 1e4, 8000)])
@@ -139,6 +139,29 @@ def test_planet_rv_all_parameterisations():
         Mabs = (2 * np.pi / P)[:, None] * np.abs(t[None, :] + 2.5e6)
         tol = 1e-10 * K[:, None] + 4e-16 * Mabs * K[:, None] / (1 - 0.97)
         assert np.all(np.abs(rv[~bad] - ref[~bad]) <= tol[~bad]), par
+
+
+def test_planet_rv_long_baseline_short_period():
+    """The epoch loop reduces the orbital phase u = (t - Tp) / P (u - rint(u) exact) instead of
+    M: short periods over long baselines (|u| up to 1e5 orbits, BJD-scale times) and both
+    seed paths (e <= 0.18 series, e > 0.18 Halley) against the C oracle's Planet.radial_velocity,
+    with the file's per-epoch tolerance (the |M| eps term is the reference's own rounding)."""
+    from oracle import oracle
+    from ravest_amd.engine import RVEngine
+    rng = np.random.default_rng(21)
+    t = np.sort(rng.uniform(0.0, 40000.0, 1500)) + 2450000.0
+    rows = []
+    for P, e in [(0.37, 0.0), (0.8, 0.05), (1.3, 0.15), (2.9, 0.18), (0.55, 0.3), (7.7, 0.6), (11.0, 0.93)]:
+        rows.append([P, rng.uniform(5, 50), e, rng.uniform(-np.pi, np.pi), 2450000.0 + rng.uniform(0, P)])
+    prm = np.array(rows)
+    eng = RVEngine(t, np.zeros_like(t), np.ones_like(t), n_planets=1, parameterisation="P K e w Tp", t0=0.0)
+    rv = eng.predict(np.concatenate([prm, np.zeros((len(prm), 4))], axis=1), t, trend=False)
+    for k, p5 in enumerate(prm):
+        ref = oracle.planet_rv(0, p5, t)
+        P, K, e = p5[0], p5[1], p5[2]
+        Mabs = 2 * np.pi / P * np.abs(t - p5[4])
+        tol = 1e-10 * K + 4e-16 * Mabs * K / (1 - e)
+        assert np.all(np.abs(rv[k] - ref) <= tol), (P, e, np.max(np.abs(rv[k] - ref) / tol))
 
 
 def test_compute_rv_dispatch():
