@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs 
     const int D = pd.n_free;
     const RunArgs &run = *runp;
     const double *x = run.x, a = run.a;
+    const RowPre pre = row_pre(pd);
     for (long long j = (long long)blockIdx.x * kWavesPerBlock + wv; j < H; j += (long long)gridDim.x * kWavesPerBlock) {
         const Draw d = draw(run, step, half, j, H);
         const double zt = (a - 1.0) * d.zu + 1.0;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs 
             q[j * D + c] = v;
         }
         wave_lds_sync();
-        const double v = post_row_wave(pd, L, full + j * pd.p_full);
+        const double v = post_row_wave(pd, L, full + j * pd.p_full, pre);
         if (lane == 0) {
             lp[j] = v;
             fac[j] = ((double)D - 1.0) * log(z);

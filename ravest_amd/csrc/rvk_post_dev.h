@@ -170,13 +170,47 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-inline __device__ double post_row_wave(const PostDev &pd, PostWaveLds &L, double *__restrict__ full) {
+// The posterior's per-lane constants for one row (column c = lane: its free position and
+// fixed value; prior slot k = lane), when p_full <= 64 and n_prior <= 64: loaded once per
+// kernel by row_pre() so their latency is off each proposal's dependent chain.
+struct RowPre {
+    bool on;
+    int f;
+    double t;
+    PriorSlot s;
+};
+
+inline __device__ RowPre row_pre(const PostDev &pd) {
     const int lane = threadIdx.x & 63;
-    for (int c = lane; c < pd.p_full; c += 64) {
-        const int f = pd.colmap[c];
-        const double v = f >= 0 ? L.x[f] : pd.tmpl[c];
-        L.f[c] = v;
-        full[c] = v;
+    RowPre r{};
+    r.on = pd.p_full <= 64 && pd.n_prior <= 64;
+    r.f = -1;
+    if (r.on) {
+        if (lane < pd.p_full) {
+            r.f = pd.colmap[lane];
+            r.t = pd.tmpl[lane];
+        }
+        if (lane < pd.n_prior) r.s = pd.slots[lane];
+    }
+    return r;
+}
+
+inline __device__ double post_row_wave(const PostDev &pd, PostWaveLds &L, double *__restrict__ full,
+                                       const RowPre &pre = RowPre{}) {
+    const int lane = threadIdx.x & 63;
+    if (pre.on) {
+        if (lane < pd.p_full) {
+            const double v = pre.f >= 0 ? L.x[pre.f] : pre.t;
+            L.f[lane] = v;
+            full[lane] = v;
+        }
+    } else {
+        for (int c = lane; c < pd.p_full; c += 64) {
+            const int f = pd.colmap[c];
+            const double v = f >= 0 ? L.x[f] : pd.tmpl[c];
+            L.f[c] = v;
+            full[c] = v;
+        }
     }
     wave_lds_sync();
     const int jit0 = 5 * pd.n_planets + pd.n_inst;
@@ -188,10 +222,17 @@ inline __device__ double post_row_wave(const PostDev &pd, PostWaveLds &L, double
         dead |= !ok;                                                                // ValueError -> -inf
     }
     wave_lds_sync();
-    for (int k = lane; k < pd.n_prior; k += 64) {
-        const PriorSlot &s = pd.slots[k];
-        const double v = s.src >= 0 ? L.f[s.src] : L.def[-s.src - 1];
-        L.term[k] = prior_lp(s, v);
+    if (pre.on) {
+        if (lane < pd.n_prior) {
+            const double v = pre.s.src >= 0 ? L.f[pre.s.src] : L.def[-pre.s.src - 1];
+            L.term[lane] = prior_lp(pre.s, v);
+        }
+    } else {
+        for (int k = lane; k < pd.n_prior; k += 64) {
+            const PriorSlot &s = pd.slots[k];
+            const double v = s.src >= 0 ? L.f[s.src] : L.def[-s.src - 1];
+            L.term[k] = prior_lp(s, v);
+        }
     }
     wave_lds_sync();
     dead = __builtin_amdgcn_ballot_w64(dead) != 0;
