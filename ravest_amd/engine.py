@@ -13,7 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .param import Parameterisation
+from .param import Parameterisation, as_parameterisation
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -27,8 +27,7 @@ class RVEngine:
     def __init__(self, time, vel, velerr, inst_idx=None, n_inst: int = 1, n_planets: int = 1,
                  parameterisation="P K e w Tp", t0: float = 0.0, device: int = -1):
         L = _lib.load()
-        if isinstance(parameterisation, str):
-            parameterisation = Parameterisation(parameterisation)
+        parameterisation = as_parameterisation(parameterisation)   # str, ours or ravest's own object
         self.parameterisation = parameterisation
         model_only = time is None                     # rvk_predict only (n_epochs = 0)
         self.time = np.zeros(0) if model_only else np.ascontiguousarray(time, np.float64)

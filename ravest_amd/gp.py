@@ -21,7 +21,7 @@ from typing import Dict, List
 import numpy as np
 
 from . import _lib
-from .param import Parameterisation, full_param_names
+from .param import Parameterisation, as_parameterisation, full_param_names
 
 SUPPORTED_KERNELS = ["Quasiperiodic"]
 HYPERPARAMS = ["gp_amp", "gp_lambda_e", "gp_lambda_p", "gp_period"]   # gp.py:37, the C-ABI hyper row order
@@ -93,8 +93,7 @@ class GPLogLikelihood:
 
     def __init__(self, time, vel, velerr, t0, instrument, unique_instruments, planet_letters,
                  parameterisation: Parameterisation, gp_kernel: GPKernel, device: int = -1) -> None:
-        if isinstance(parameterisation, str):
-            parameterisation = Parameterisation(parameterisation)
+        parameterisation = as_parameterisation(parameterisation)   # str, ours or ravest's own object
         if gp_kernel.kernel_type != "Quasiperiodic":
             raise ValueError(f"no device form for GP kernel {gp_kernel.kernel_type}")
         self.time, self.vel, self.velerr, self.t0 = time, vel, velerr, t0

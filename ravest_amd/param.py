@@ -179,8 +179,26 @@ class Parameterisation:
         return ~(P <= 0) & ~(K <= 0) & ~(e < 0) & ~(e >= 1.0) & ((-np.pi <= w) & (w < np.pi))
 
 
+def as_parameterisation(obj) -> Parameterisation:
+    """The drop-in boundary for parameterisations: a string, this module's class, or ravest's
+    own ``Parameterisation`` -- or any object with its public ``.parameterisation`` string
+    (src/ravest/param.py:129-151; ravest's class has no ``.code`` or vectorised forms, so
+    it is re-expressed here from that string, with the reference's ValueError for an
+    unknown one)."""
+    if isinstance(obj, Parameterisation):
+        return obj
+    if isinstance(obj, str):
+        return Parameterisation(obj)
+    name = getattr(obj, "parameterisation", None)
+    if isinstance(name, str):
+        return Parameterisation(name)
+    raise TypeError(f"{obj!r} is not a parameterisation: expected a string or an object with a "
+                    "'.parameterisation' string (ravest.param.Parameterisation)")
+
+
 def full_param_names(planet_letters, parameterisation: Parameterisation, unique_instruments) -> list:
     """Full parameter order of the C-ABI ``theta`` row (include/rvk.h)."""
+    parameterisation = as_parameterisation(parameterisation)
     names = [f"{par}_{L}" for L in planet_letters for par in parameterisation.pars]
     names += [f"g_{s}" for s in unique_instruments]
     names += [f"jit_{s}" for s in unique_instruments]

@@ -24,8 +24,8 @@ from typing import Callable, Dict
 import numpy as np
 
 from . import _lib
-from .param import Parameterisation, full_param_names
-from .prior import Uniform, device_params, logpdf_vec
+from .param import Parameterisation, as_parameterisation, full_param_names
+from .prior import Uniform, as_priors, device_params, logpdf_vec
 
 
 class LogLikelihood:
@@ -40,7 +40,7 @@ class LogLikelihood:
         self.unique_instruments = unique_instruments
         self.t0 = t0
         self.planet_letters = planet_letters
-        self.parameterisation = parameterisation
+        self.parameterisation = as_parameterisation(parameterisation)
         # fit.py:3585-3598
         _inst_to_idx = {inst: i for i, inst in enumerate(self.unique_instruments)}
         self._instrument_indices = np.array([_inst_to_idx[inst] for inst in self.instrument], dtype=np.int32)
@@ -79,7 +79,8 @@ class LogPrior:
     """fit.py:3663-3691."""
 
     def __init__(self, priors: dict) -> None:
-        self.priors = priors
+        self.priors = priors                  # the caller's objects: the scalar path calls them
+        self._vec = as_priors(priors)         # ravest's built-ins re-expressed for the batch path
 
     def __call__(self, params: Dict[str, float]) -> float:
         log_prior_probability = 0
@@ -91,7 +92,7 @@ class LogPrior:
         """Same sum, same key order, vectorised over walkers."""
         lp = 0
         for param, col in cols.items():
-            lp = lp + logpdf_vec(self.priors[param], col)
+            lp = lp + logpdf_vec(self._vec[param], col)
         return lp
 
 
@@ -102,8 +103,9 @@ class LogPosterior:
                  fixed_params: dict, free_params_names: list, time, vel, velerr, instrument,
                  unique_instruments, t0: float, engine=None, device: int = -1) -> None:
         self.planet_letters = planet_letters
-        self.parameterisation = parameterisation
+        self.parameterisation = as_parameterisation(parameterisation)   # ravest's own object accepted
         self.priors = priors
+        self._priors = as_priors(priors)      # ravest's prior objects accepted (prior.as_prior)
         self.fixed_params = fixed_params
         self.free_params_names = free_params_names
         self.time = time
@@ -114,7 +116,7 @@ class LogPosterior:
         self.t0 = t0
         self.log_likelihood = LogLikelihood(time=time, vel=vel, velerr=velerr, instrument=instrument,
                                             unique_instruments=unique_instruments, t0=t0,
-                                            planet_letters=planet_letters, parameterisation=parameterisation,
+                                            planet_letters=planet_letters, parameterisation=self.parameterisation,
                                             engine=engine, device=device)
         self.log_prior = LogPrior(self.priors)
         (self._logprob_jacobian_correction, self._logprob_prior_renorm_correction,
@@ -130,7 +132,7 @@ class LogPosterior:
         secosw_key, sesinw_key = f"secosw_{letter}", f"sesinw_{letter}"
         e_key, w_key = f"e_{letter}", f"w_{letter}"
         if secosw_key in self.priors and sesinw_key in self.priors:
-            sp, vp = self.priors[secosw_key], self.priors[sesinw_key]
+            sp, vp = self._priors[secosw_key], self._priors[sesinw_key]
             if (isinstance(sp, Uniform) and isinstance(vp, Uniform) and sp.lower == -1 and sp.upper == 1
                     and vp.lower == -1 and vp.upper == 1):
                 return "CASE_2"
@@ -289,7 +291,7 @@ class DevicePosterior:
         conv_keys = {f"{dp}_{L}": (i, j) for i, L in enumerate(lpost.planet_letters)
                      for j, dp in enumerate(("P", "K", "e", "w", "Tp"))}
         for k in lpost._prior_order:
-            kind, p = device_params(lpost.priors[k])
+            kind, p = device_params(lpost._priors[k])
             kinds.append(kind)
             pars.append(p)
             if lpost._case3 and k in conv_keys:

@@ -17,14 +17,13 @@ from __future__ import annotations
 import numpy as np
 
 from .engine import RVEngine
-from .param import Parameterisation, full_param_names
+from .param import Parameterisation, as_parameterisation, full_param_names
 
 
 class PosteriorPredictive:
     def __init__(self, planet_letters, parameterisation: Parameterisation, fixed_params: dict,
                  free_params_names: list, unique_instruments, t0: float, device: int = -1) -> None:
-        if isinstance(parameterisation, str):
-            parameterisation = Parameterisation(parameterisation)
+        parameterisation = as_parameterisation(parameterisation)   # str, ours or ravest's own object
         self.planet_letters = list(planet_letters)
         self.parameterisation = parameterisation
         self.fixed_params = dict(fixed_params)

@@ -238,6 +238,36 @@ class Beta:
         return f"Beta(a={self.a}, b={self.b})"
 
 
+# Public constructor attributes of ravest's built-in priors (src/ravest/prior.py:39-488): a
+# prior object of the reference's own classes is re-expressed from exactly these, so the
+# derived constants (_log_norm_const, _a/_b, _log_beta) come from this module's
+# constructors, i.e. the reference's expressions, never from another object's privates.
+PUBLIC_ATTRS = {"Uniform": ("lower", "upper"), "EccentricityUniform": ("upper",), "Normal": ("mean", "std"),
+                "TruncatedNormal": ("mean", "std", "lower", "upper"), "HalfNormal": ("std",),
+                "Rayleigh": ("scale",), "VanEylen19Mixture": ("sigma_normal", "sigma_rayleigh", "f"),
+                "Beta": ("a", "b")}
+
+
+def as_prior(prior):
+    """The drop-in boundary for priors: an instance of this module's classes is returned as is;
+    an object whose class is named like one of ravest's built-in priors and carries that
+    prior's public attributes (ravest.prior.Uniform(lower, upper), ...) becomes the
+    equivalent built-in here (same validation, same formulas); anything else is a custom
+    callable and stays one (host path, evaluated per walker like the reference)."""
+    if isinstance(prior, _BUILTIN):
+        return prior
+    name = type(prior).__name__
+    attrs = PUBLIC_ATTRS.get(name)
+    if attrs is not None and all(hasattr(prior, a) for a in attrs):
+        return globals()[name](*(getattr(prior, a) for a in attrs))
+    return prior
+
+
+def as_priors(priors: dict) -> dict:
+    """``as_prior`` over a priors dict, keeping its key order (the reference sums in it)."""
+    return {k: as_prior(v) for k, v in priors.items()}
+
+
 def logpdf_vec(prior, x) -> np.ndarray:
     """Vectorised log-prior for any prior: built-ins use ``logpdf``; user callables are
     evaluated per element (the reference's per-walker semantics)."""
@@ -245,6 +275,9 @@ def logpdf_vec(prior, x) -> np.ndarray:
         return prior.logpdf(x)
     x = _arr(x)
     return np.array([float(prior(float(v))) for v in x.ravel()]).reshape(x.shape)
+
+
+_BUILTIN = (Uniform, EccentricityUniform, Normal, TruncatedNormal, HalfNormal, Rayleigh, VanEylen19Mixture, Beta)
 
 
 # ---- device form (include/rvk_post.h RVK_PRIOR_*) --------------------------------------------
@@ -262,6 +295,7 @@ def device_params(prior):
     one of the built-in classes raises NotImplementedError: custom callables stay on the
     host path (posterior.LogPosterior.log_probability_batch)."""
     from . import _lib
+    prior = as_prior(prior)
     p = np.zeros(_lib.PRIOR_NPAR)
     name = type(prior).__name__
     if isinstance(prior, Uniform):

@@ -112,3 +112,14 @@ def test_device_sampler_nan_raises():
     s = DeviceEnsembleSampler(lpost, 16, seed=1)
     with pytest.raises(ValueError):
         s.run_mcmc(x0, 2)
+
+
+@pytest.mark.parametrize("name", logpost_cases())
+def test_device_posterior_from_foreign_objects(name):
+    """Built from ravest's OWN object types (tests/_foreign.py stand-ins: only the reference's
+    public attributes), the device and host log-posteriors still equal the reference goldens."""
+    from tests import _foreign as F
+    case = load_case(name)
+    lpost = LogPosterior(*F.posterior_args(case))
+    assert_ll_close(lpost.device_posterior()(case["theta_free"]), case["log_prob"], what=f"foreign-device-{name}")
+    assert_ll_close(lpost.log_probability_batch(case["theta_free"]), case["log_prob"], what=f"foreign-host-{name}")
