@@ -48,13 +48,14 @@ def parse():
     ap.add_argument("--streams", type=int, default=1, help="independent streams per graph")
     ap.add_argument("--no-gp", action="store_true", help="skip the config-5 GP likelihood measurement")
     ap.add_argument("--no-predictive", action="store_true", help="skip the posterior-predictive measurement")
+    ap.add_argument("--no-configs", action="store_true", help="skip the config-3 / config-4 sub-measurements")
     return ap.parse_args()
 
 
 def cpu_baseline(ds, theta, budget_s):
     """Time the C oracle (oracle/rv_oracle.c, OpenMP over walkers) on a bounded sample."""
     from oracle import oracle
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     n_ep, n_pl = len(ds.time), len(ds.planet_letters)
     sample = theta[: min(len(theta), 4096)]
     oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), n_pl,
@@ -88,6 +89,7 @@ def cpu_baseline(ds, theta, budget_s):
             r2 += 1
     el2 = time.perf_counter() - t2
     return {"value": solves / el, "unit": "Kepler solves/s", "cores": used, "kind": "port",
+            "host_cpus": host_cpu_info(),
             "sample": f"{reps} x {len(sample)} walkers x {n_ep} epochs x {n_pl} planet(s) of the same "
                       f"config-{ds.cfg} ensemble, C oracle (oracle/rv_oracle.c, fp64, OpenMP), {el:.1f} s",
             "single_core_value": r1 * len(one) * n_ep * n_pl / el1,
@@ -96,29 +98,188 @@ def cpu_baseline(ds, theta, budget_s):
                             f"{el2:.1f} s"}
 
 
+def host_threads() -> int:
+    """Threads for the CPU baseline: every CPU this process may run on (sched_getaffinity),
+    but no more than the job's CPU share when the launcher states one (OMP_NUM_THREADS: the
+    GPU pool sets it to the 16 CPUs one GPU's job may use; its nproc shows the whole host)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
+def host_cpu_info() -> dict:
+    return {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "threads_used": host_threads()}
+
+
 def agreement(ds, theta, ll, world, k: int = 512) -> dict:
     """Log-prob agreement of the measured kernel's output with the C restatement of the reference
     (oracle/rv_oracle.c, pinned to the reference's golden vectors) on the first k walkers of this
     rank, against the stated fp64 tolerance |d| <= 1e-9 max(1, |ref|) and an identical -inf mask;
-    for N > 1 the all-gathered block was also checked bitwise against each rank's own result."""
+    for N > 1, `ranks_bitwise_identical` is set by main(): the all-gathered block of every rank's
+    results against rank 0's own single evaluation of all N x W walkers."""
     from oracle import oracle
     ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments),
                             len(ds.planet_letters), ds.parameterisation.code, ds.t0, theta[:k],
-                            nthreads=min(16, os.cpu_count() or 1))
+                            nthreads=host_threads())
     got = ll[:k]
     fin = np.isfinite(ref)
     rel = np.abs(got[fin] - ref[fin]) / np.maximum(1.0, np.abs(ref[fin]))
     return {"walkers_checked": int(k), "mask_identical": bool(np.array_equal(np.isfinite(got), fin)),
             "max_rel_err": float(rel.max()) if rel.size else 0.0, "tolerance": 1e-9,
-            "ranks_bitwise_identical": True if world > 1 else None}
+            "ranks_bitwise_identical": None}
 
 
-def load_pmc(cfg):
-    p = os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json")
+# MI355X VALU issue costs (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost' / SIMD-32: a wave64
+# instruction issues over 2 cycles; fp64 runs at half the fp32 rate -> 4; transcendentals 8 (f32),
+# 16 (f64, assumed at the same 1/2 ratio)); 1024 SIMDs at 2.4 GHz.
+N_SIMD, CLOCK_HZ = 1024, 2.4e9
+
+
+def valu_roofline(pmc: dict | None, kern_ms: float) -> dict | None:
+    """The binding resource of the likelihood kernel: fp64 VALU.  From the PMC counters of the
+    same kernel (profiles/pmc_config<N>.json, separate rocprofv3 --pmc passes): the fp64 FLOP
+    rate against the 78.6 TF fp64 vector peak, and an issue-cycle estimate (instructions x
+    their SIMD issue cycles / (1024 SIMDs x 2.4 GHz x kernel time))."""
+    if not pmc:
+        return None
+    c = pmc.get("counters_per_launch", {})
+    if not c.get("SQ_INSTS_VALU_FLOPS_FP64"):
+        return None
+    t = kern_ms * 1e-3
+    f64 = c["SQ_INSTS_VALU_FLOPS_FP64"] * 64 / t / 1e12     # per-wave-instruction FLOP count x 64 lanes
+    f32 = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * 64 / t / 1e12
+    n64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
+    tr64, tr32 = c.get("SQ_INSTS_VALU_TRANS_F64", 0.0), c.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+    other = max(0.0, c.get("SQ_INSTS_VALU", 0.0) - n64 - tr64 - tr32)
+    cycles = 4 * n64 + 16 * tr64 + 8 * tr32 + 2 * other
+    return {"bound": "valu-fp64", "fp64_tflops": f64, "peak_fp64_tflops": FP64_VECTOR_PEAK_TF,
+            "fp64_flop_frac": f64 / FP64_VECTOR_PEAK_TF, "fp32_tflops": f32,
+            "issue_cycle_frac_est": cycles / (N_SIMD * CLOCK_HZ * t),
+            "valu_insts_per_launch": c.get("SQ_INSTS_VALU"), "kernel": pmc.get("kernel"),
+            "source": (pmc.get("source") or "") + " (profiles/%s)" % pmc.get("_file", "")}
+
+
+def load_pmc_file(name):
+    p = os.path.join(ROOT, "profiles", name)
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f)
+            d = json.load(f)
+        d["_file"] = name
+        return d
     return None
+
+
+def graph_kernel_ms(launch, G: int = 20, reps: int = 10) -> float:
+    """Average duration of `launch(stream)` (one kernel launch) inside G-launch HIP graph replays,
+    HIP events on the replay stream, median over reps."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cap = torch.cuda.Stream(dev)
+    for _ in range(3):
+        launch(cap)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        for _ in range(G):
+            launch(cap)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    st = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record(st)
+        g.replay()
+        b.record(st)
+    torch.cuda.synchronize(dev)
+    return float(np.median([a.elapsed_time(b) for a, b in evs])) / G
+
+
+def config_line(cfg: int, W: int | None = None, label: str | None = None) -> dict:
+    """One more BASELINE config on this GPU (theta resident in HBM): kernel ms (HIP events around
+    graph replays), Kepler solves/s, the algorithmic-HBM and fp64-VALU rooflines, and log-prob
+    agreement with the C oracle on 512 walkers."""
+    import torch
+    from ravest_amd.engine import RVEngine
+    from ravest_amd.synth import make_config
+    ds = make_config(cfg, n_walkers=W)
+    ds.cfg = cfg
+    W = len(ds.theta)
+    n_ep, n_pl = len(ds.time), len(ds.planet_letters)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), n_pl, ds.parameterisation,
+                   ds.t0, device=dev.index)
+    th = torch.from_numpy(ds.theta).to(dev)
+    out = torch.empty(W, dtype=torch.float64, device=dev)
+    ms = graph_kernel_ms(lambda st: eng.loglike_device(th, out, st))
+    torch.cuda.synchronize(dev)
+    ll = out.cpu().numpy()
+    alg = W * (n_ep * BYTES_PER_WALKER_EPOCH + ds.theta.shape[1] * 8 + 8)
+    gbs = alg / (ms * 1e-3) / 1e9
+    pmc = load_pmc_file(f"pmc_{label or 'config%d' % cfg}.json")
+    return {"config": f"config {cfg}: {n_pl} planet(s), {n_ep} epochs, {W} walkers, {len(ds.unique_instruments)} "
+                      f"instrument(s), fp64, theta resident in HBM",
+            "kernel_ms": ms, "kepler_solves_per_s": W * n_ep * n_pl / (ms * 1e-3),
+            "walker_evals_per_s": W / (ms * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                         "valu": valu_roofline(pmc, ms)},
+            "n_masked_walkers": int((~np.isfinite(ll)).sum()),
+            "logprob_agreement": agreement(ds, ds.theta, ll, 1)}
+
+
+def config4_sharded_line(world: int, rank: int, backend: str, reps: int = 20) -> dict:
+    """Config 4 as BASELINE names it: 65536 walkers (2 planets x 512 epochs) split over the N
+    ranks (strong scaling, 65536/N contiguous walkers each) by ShardedDevicePosterior: each rank
+    launches rvk_loglike_device on its slice and the per-walker log-probs are all-gathered (RCCL
+    over xGMI) into every rank's [65536] buffer.  Timed: reps x (launch + all-gather), barrier +
+    sync on both sides, max over ranks.  Checked: the gathered block equals rank 0's own single
+    evaluation of all 65536 walkers, bit for bit."""
+    import torch
+    import torch.distributed as dist
+    from ravest_amd.distributed import ShardedDevicePosterior
+    from ravest_amd.engine import RVEngine
+    from ravest_amd.synth import make_config
+    ds = make_config(4)
+    Wt = len(ds.theta)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), len(ds.planet_letters),
+                   ds.parameterisation, ds.t0, device=dev.index)
+    th = torch.from_numpy(ds.theta).to(dev)
+    out = torch.empty(Wt, dtype=torch.float64, device=dev)
+    if world > 1 and backend != "nccl":
+        return {"skipped": "gloo rehearsal: the device-resident all-gather needs RCCL (backend nccl)"}
+    sh = ShardedDevicePosterior(eng.loglike_device)
+    for _ in range(3):
+        sh(th, out)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sh(th, out)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ref = torch.empty(Wt, dtype=torch.float64, device=dev)
+    eng.loglike_device(th, ref)
+    torch.cuda.synchronize(dev)
+    same = bool(np.array_equal(ref.cpu().numpy(), out.cpu().numpy()))
+    if world > 1:
+        t = torch.tensor([el, 0.0 if same else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, same = float(t[0]), bool(t[1] == 0.0)
+    n_ep, n_pl = len(ds.time), len(ds.planet_letters)
+    solves = Wt * n_ep * n_pl * reps
+    return {"config": f"config 4: {n_pl} planets, {n_ep} epochs, {Wt} walkers sharded over {world} GPU(s) "
+                      f"({Wt // world} per rank), RCCL all-gather of the log-probs into every rank",
+            "ms_per_eval": el / reps * 1e3, "kepler_solves_per_s": solves / el, "walker_evals_per_s": Wt * reps / el,
+            "scaling": "strong", "n_gpus": world,
+            "bitwise_identical_to_single_gpu": same}
 
 
 def sampler_line(W: int, steps: int = 256) -> dict:
@@ -205,7 +366,7 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     return {"config": f"config 5: 1 planet + quasi-periodic GP, {n} epochs, {W} walkers, fp32 factorisation",
             "ms_per_eval": ms, "walker_evals_per_s": W / (ms * 1e-3),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                         "frac": tf / FP32_MFMA_PEAK_TF, "traffic": (load_pmc(5) or {}).get("hbm_bytes_per_launch"),
+                         "frac": tf / FP32_MFMA_PEAK_TF, "traffic": (load_pmc_file("pmc_config5.json") or {}).get("hbm_bytes_per_launch"),
                          "note": "algorithmic FLOP = W*(n^3/3 + 2n^2) per launch / launch duration; traffic = "
                                  "L2 memory-side bytes per launch (PMC, profiles/pmc_config5.json; includes "
                                  "Infinity-Cache hits: the workspace tiles re-read by the left-looking update)"},
@@ -376,10 +537,21 @@ def main():
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
-        # the gathered block is every rank's result, bitwise: check rank 0's slice on rank 0
-        mine = gath[(r - 1) % nset].view(world, G, W)[rank, G - 1].cpu().numpy()
-        if not np.array_equal(mine, ll):
-            raise RuntimeError("all-gathered log-probs differ from the local result")
+    ranks_same = None
+    if world > 1:
+        # every rank's results, as gathered, against THIS rank's own single launch over all
+        # world x W walkers (a different batch size, so possibly a different lane layout):
+        # bitwise identical means the shard split changes nothing
+        got = gath[(r - 1) % nset].view(world, G, W)[:, G - 1, :].reshape(-1).cpu().numpy()
+        th_all = torch.from_numpy(theta_all).to(dev)
+        ref_all = torch.empty(world * W, dtype=torch.float64, device=dev)
+        eng.loglike_device(th_all, ref_all, stream)
+        torch.cuda.synchronize(dev)
+        bad = 0.0 if np.array_equal(got, ref_all.cpu().numpy()) else 1.0
+        t = torch.tensor([bad], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ranks_same = bool(t[0] == 0.0)
+        del th_all, ref_all
     args.steps = steps_run
 
     solves = W * n_ep * n_pl * args.steps * world
@@ -387,19 +559,9 @@ def main():
     if rank == 0:
         alg_bytes = W * (n_ep * BYTES_PER_WALKER_EPOCH + theta.shape[1] * 8 + 8)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        pmc = load_pmc(args.config)
-        traffic = None
-        valu = None
-        if pmc:
-            traffic = pmc.get("hbm_bytes_per_launch")
-            c = pmc.get("counters_per_launch", {})
-            if c.get("SQ_INSTS_VALU_FLOPS_FP64"):
-                # FLOPS counters count per wave instruction (FMA = 2): x64 lanes -> FLOP per launch
-                f64 = c["SQ_INSTS_VALU_FLOPS_FP64"] * 64 / (kern_ms * 1e-3) / 1e12
-                f32 = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * 64 / (kern_ms * 1e-3) / 1e12
-                valu = {"fp64_tflops": f64, "peak_fp64_tflops": FP64_VECTOR_PEAK_TF, "frac": f64 / FP64_VECTOR_PEAK_TF,
-                        "fp32_tflops": f32, "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
-                        "source": pmc.get("source") + " (profiles/pmc_config%d.json)" % args.config}
+        pmc = load_pmc_file(f"pmc_config{args.config}.json")
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        valu = valu_roofline(pmc, kern_ms)
         line = {
             "metric": "walker-log-prob evals/sec (= Kepler solves/sec) at 1/2/4/8 MI355X",
             "value": value, "unit": "Kepler solves/s", "n_gpus": world, "steps": args.steps,
@@ -418,13 +580,19 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "achieved_per_step": alg_bytes / (el / args.steps) / 1e9,
-                         "note": "algorithmic bytes = W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY §8(d)) / "
-                                 "average kernel duration (HIP events around each G-launch graph replay in the "
-                                 "timed region / G); the kernel is fp64-VALU bound, see 'valu'"},
-            "valu": valu,
+                         "valu": valu,
+                         "note": "achieved = algorithmic bytes W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY "
+                                 "§8(d)) / average kernel duration (HIP events around each G-launch graph replay "
+                                 "in the timed region / G); traffic = PMC HBM bytes per launch (the epoch arrays "
+                                 "are re-read from L2/MALL, not HBM). The binding resource is fp64 VALU issue: "
+                                 "'valu' (PMC counters of the same kernel)."},
         }
         line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
         line["logprob_agreement"] = agreement(ds, theta, ll, world)
+        line["logprob_agreement"]["ranks_bitwise_identical"] = ranks_same
+        if world == 1 and args.config == 2 and not args.no_configs:
+            line["config3"] = config_line(3)
+            line["config4_shard"] = config_line(4, W=8192)
         if world == 1 and not args.no_sampler:
             line["sampler"] = sampler_line(W)
         if world == 1 and not args.no_gp:
@@ -433,6 +601,11 @@ def main():
             line["predictive"] = predictive_line(eng, theta)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
+    if not args.no_configs:
+        c4 = config4_sharded_line(world, rank, backend)      # collective: every rank takes part
+        if rank == 0:
+            line["config4_sharded"] = c4
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

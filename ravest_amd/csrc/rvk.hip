@@ -363,31 +363,27 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
             PlanetK pk[NP];
 #pragma unroll
             for (int p = 0; p < NP; ++p) pk[p] = pks[j][p];
-            double chi2 = 0.0, prod = 0.5;
-            int expo = 1;
-            auto epochs = [&](auto trend_c) {
+            // A = 64 / LPW accumulators per lane: accumulator a of lane li holds exactly what lane
+            // li + LPW a of the one-wave-per-walker kernel holds (epochs li + LPW a + 64 k, in
+            // order), and the segment total is formed from their 16-lane row sums in that
+            // kernel's order ((r0 + r1) + (r2 + r3)) -- so a walker's log-likelihood has the same
+            // bits whatever the layout, batch size or shard (tests/test_gpu_layout.py).
+            constexpr int A = 64 / LPW;
+            auto one_acc = [&](int vl, double t_f, double v_f, double s_f, int i_f, auto trend_c) -> double {
                 constexpr bool TREND = decltype(trend_c)::value;
-                double tn = t_1, vn = v_1, sn = s_1;
-                int in_ = i_1;
-#if RVK_EPOCH_OFF32
-                // off = 8 (i + LPW): the only induction variable (as in loglike_kernel)
+                double chi2 = 0.0, prod = 0.5;   // prod * 2^expo = running product of s^2
+                int expo = 1;
+                double tn = t_f, vn = v_f, sn = s_f;
+                int in_ = i_f;
+                // off = 8 (i + 64), the next epoch's byte offset (as in loglike_kernel)
                 const unsigned lim = 8u * (unsigned)n_epochs;
-                for (unsigned off = 8u * (unsigned)(li + LPW); off < lim + 8u * LPW; off += 8u * LPW) {
+                for (unsigned off = 8u * (unsigned)(vl + 64); off < lim + 512u; off += 512u) {
                     const double t = tn, vel = vn, s2b = sn;
                     const int ii = in_;
                     if (off < lim) {
                         tn = ld_off(d.t, off); vn = ld_off(d.vel, off); sn = ld_off(d.s2, off);
                         if (MULTI) in_ = ld_off(d.inst, off >> 1);
                     }
-#else
-                for (int i = li; i < n_epochs; i += LPW) {
-                    const double t = tn, vel = vn, s2b = sn;
-                    const int ii = in_;
-                    if (i + LPW < n_epochs) {
-                        tn = d.t[i + LPW]; vn = d.vel[i + LPW]; sn = d.s2[i + LPW];
-                        if (MULTI) in_ = d.inst[i + LPW];
-                    }
-#endif
                     double gam = g0, jj = j0sq;
                     if (MULTI) {
                         for (int k = 1; k < n_inst; ++k) {
@@ -409,24 +405,48 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
                     prod = __builtin_frexp(prod, &ex);
                     expo += ex;
                 }
+                double lsum = log_frexp(prod, expo);
+                if (!(prod >= 0.5 && prod < 1.0)) lsum = prod == 0.0 ? -INFINITY : prod;
+                return chi2 + lsum;
             };
-            if (ok) {
-                if (__builtin_amdgcn_ballot_w64((gd != 0.0) | (gdd != 0.0))) epochs(std::true_type{});
-                else epochs(std::false_type{});
+            // R[r][k]: row r of segment k's one-wave layout (its lanes 16r .. 16r+15), which is
+            // accumulator 16r / LPW at segment offset 16r % LPW.  The accumulators run one after
+            // another (a runtime loop: one copy of the epoch loop, no extra live state but the
+            // uniform row sums).
+            constexpr int RPA = LPW / 16;                        // rows per accumulator
+            double R[4][SEG];
+            const bool trend = __builtin_amdgcn_ballot_w64((gd != 0.0) | (gdd != 0.0)) != 0;
+#pragma unroll 1
+            for (int a = 0; a < A; ++a) {
+                const int vl = li + LPW * a;                     // the one-wave kernel's lane
+                double t_f = t_1, v_f = v_1, s_f = s_1;
+                int i_f = i_1;
+                if (a > 0) {
+                    t_f = 0.0; v_f = 0.0; s_f = 1.0; i_f = 0;
+                    if (vl < n_epochs) {
+                        t_f = d.t[vl]; v_f = d.vel[vl]; s_f = d.s2[vl];
+                        if (MULTI) i_f = d.inst[vl];
+                    }
+                }
+                double x = 0.0;
+                if (ok) {
+                    if (trend) x = one_acc(vl, t_f, v_f, s_f, i_f, std::true_type{});
+                    else x = one_acc(vl, t_f, v_f, s_f, i_f, std::false_type{});
+                }
+                x = row_sum(x);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (r / RPA == a) {
+#pragma unroll
+                        for (int k = 0; k < SEG; ++k) R[r][k] = readlane_d(x, k * LPW + 16 * (r % RPA));
+                    }
+                }
             }
-            double lsum = log_frexp(prod, expo);
-            if (!(prod >= 0.5 && prod < 1.0)) lsum = prod == 0.0 ? -INFINITY : prod;
-            const double v = row_sum(ok ? chi2 + lsum : 0.0);
             const unsigned long long okm = __builtin_amdgcn_ballot_w64(ok);
-            // the segment totals are read (v_readlane) in uniform control flow: inside the
-            // lane-0 branch below the compiler may sink the last butterfly add into it, and
-            // the other rows' lanes would never compute it
             double res[SEG];
 #pragma unroll
             for (int k = 0; k < SEG; ++k) {
-                double tot = readlane_d(v, k * LPW);
-#pragma unroll
-                for (int r = 1; r < LPW / 16; ++r) tot += readlane_d(v, k * LPW + 16 * r);
+                const double tot = (R[0][k] + R[1][k]) + (R[2][k] + R[3][k]);
                 res[k] = -0.5 * (tot + (double)n_epochs * kLog2Pi);
                 if (post.lp) res[k] = ((res[k] + readlane_d(lpw, k * LPW)) + post.jac) + post.renorm;
             }

@@ -64,3 +64,70 @@ class ShardedLogProbability:
         full = out.cpu().numpy().reshape(self.world, per)
         return np.concatenate([full[r, : shard_bounds(n, self.world, r)[1] - shard_bounds(n, self.world, r)[0]]
                                for r in range(self.world)])
+
+
+class ShardedDevicePosterior:
+    """Device-resident walker sharding: the config-4 form of the drop-in.
+
+    Every rank holds the same proposal block ``theta [W, D]`` in its own HBM (the stretch
+    move is replicated, or the block was broadcast once); rank r evaluates its contiguous
+    slice ``shard_bounds(W, world, r)`` with ``evaluate(theta_slice, out_slice, stream)`` --
+    ``DevicePosterior.device`` (rvk_logpost_device) or ``RVEngine.loglike_device`` on a
+    GPU, any tensor function on CPU -- and the per-walker log-probs are all-gathered
+    (``all_gather_into_tensor``: RCCL over xGMI with the "nccl" backend, gloo on CPU) into
+    ``out [W]`` on every rank.  No host staging: theta, the slices and the gathered block
+    stay device tensors.  Each walker is computed wholly on one GPU by a kernel whose
+    result does not depend on the batch it is in (tests/test_gpu_layout.py), so ``out``
+    is bitwise the single-GPU evaluation of the whole block at any world size.
+    Replaces ravest's ``pool.map`` of ``log_probability`` over walkers (fit.py:1068-1075)."""
+
+    def __init__(self, evaluate, group=None) -> None:
+        import torch.distributed as dist
+        if hasattr(evaluate, "device") and callable(getattr(evaluate, "device")):
+            evaluate = evaluate.device                    # a DevicePosterior
+        self.evaluate = evaluate
+        self.group = group
+        self.dist = dist
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._inplace = dist.get_backend(group) == "nccl"   # RCCL's in-place all-gather (send = recv + r*n)
+        self._bufs = {}
+
+    def bounds(self, n: int):
+        return shard_bounds(n, self.world, self.rank)
+
+    def _buf(self, key, n, like):
+        import torch
+        b = self._bufs.get(key)
+        if b is None or b.numel() < n or b.device != like.device:
+            b = torch.empty(n, dtype=torch.float64, device=like.device)
+            self._bufs[key] = b
+        return b[:n]
+
+    def __call__(self, theta, out=None, stream=None):
+        """theta: float64 tensor [W, >=D] (same on every rank); out: float64 [W] or None.
+        Returns out, holding every walker's log-probability on every rank."""
+        import torch
+        W = theta.shape[0]
+        if out is None:
+            out = torch.empty(W, dtype=torch.float64, device=theta.device)
+        lo, hi = self.bounds(W)
+        per = -(-W // self.world)                         # all_gather needs equal shard sizes
+        even = per * self.world == W
+        gathered = out if even else self._buf("gather", per * self.world, theta)
+        local = gathered[self.rank * per:self.rank * per + per] if even else self._buf("local", per, theta)
+        if hi > lo:
+            if stream is None:
+                self.evaluate(theta[lo:hi], local[:hi - lo])
+            else:
+                self.evaluate(theta[lo:hi], local[:hi - lo], stream)
+        if not even:
+            local[hi - lo:] = float("nan")                # padding, dropped below
+        if self.world > 1:
+            src = local if (not even or self._inplace) else local.clone()
+            self.dist.all_gather_into_tensor(gathered, src, group=self.group)
+        if not even:
+            for r in range(self.world):
+                a, b = shard_bounds(W, self.world, r)
+                out[a:b] = gathered[r * per:r * per + (b - a)]
+        return out

@@ -5,6 +5,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.multiprocessing as mp
 
 from ravest_amd.distributed import shard_bounds
@@ -39,6 +40,59 @@ def _worker(rank, world, port, q):
         q.put((rank, ok, float(s.get_chain()[-1].sum())))
     finally:
         dist.destroy_process_group()
+
+
+def _oracle_eval(ds):
+    """The injected per-shard evaluator: the C oracle on CPU tensors (the GPU run injects
+    DevicePosterior.device / RVEngine.loglike_device)."""
+    from oracle import oracle
+
+    def ev(theta, out):
+        ll, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments),
+                               len(ds.planet_letters), ds.parameterisation.code, ds.t0, theta.numpy(), nthreads=1)
+        out.copy_(torch.from_numpy(ll))
+    return ev
+
+
+def _sharded_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from ravest_amd.distributed import ShardedDevicePosterior
+    from ravest_amd.synth import make_dataset, make_walkers
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ds = make_dataset(2, 96, 2, seed=4)
+        res = {}
+        for W in (64, 37, 5):
+            theta = torch.from_numpy(make_walkers(ds, W, seed=4))
+            sh = ShardedDevicePosterior(_oracle_eval(ds))
+            res[W] = sh(theta).numpy().tolist()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_device_posterior(world):
+    """ShardedDevicePosterior itself (not a toy): every rank ends with the whole block's
+    log-probs, bitwise equal to one process evaluating all walkers, for even and ragged W."""
+    from ravest_amd.synth import make_dataset, make_walkers
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ds = make_dataset(2, 96, 2, seed=4)
+    for W in (64, 37, 5):
+        theta = torch.from_numpy(make_walkers(ds, W, seed=4))
+        ref = torch.empty(W, dtype=torch.float64)
+        _oracle_eval(ds)(theta, ref)
+        for r in range(world):
+            assert np.array_equal(np.array(res[r][W]), ref.numpy()), (W, r)
 
 
 def test_shard_bounds_cover():

@@ -7,7 +7,7 @@ OUT=${1:-gpurun_out/pmc}
 CFG=${2:-2}
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-sampler --no-gp --no-predictive"
+CMD="python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-sampler --no-gp --no-predictive --no-configs"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_WAVES" \
