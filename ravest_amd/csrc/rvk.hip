@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -682,6 +683,34 @@ int rvk::fail(int code, const std::string &msg) {
     return code;
 }
 
+int rvk::grow_dev(void **p, size_t *cap, size_t need) {
+    if (need <= *cap && *p) return RVK_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need > 0 ? need : 1));
+    *cap = need;
+    return RVK_OK;
+}
+
+int rvk::shared_table(int device, const SC **tab) {
+    static std::mutex mu;
+    static SC *tabs[64] = {};
+    if (device < 0 || device >= 64) return fail(RVK_E_ARG, "device ordinal out of range");
+    std::lock_guard<std::mutex> lk(mu);
+    if (!tabs[device]) {
+        SC *t = nullptr;
+        int rc = upload_table(&t);
+        if (rc) {
+            (void)hipFree(t);
+            return rc;
+        }
+        tabs[device] = t;
+    }
+    *tab = tabs[device];
+    return RVK_OK;
+}
+
 
 extern "C" {
 
@@ -701,15 +730,7 @@ int rvk_device_count(void) {
     return n;
 }
 
-static int grow(double **p, size_t *cap, size_t need) {
-    if (need <= *cap) return RVK_OK;
-    if (*p) HIPCHK(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    HIPCHK(hipMalloc(p, need));
-    *cap = need;
-    return RVK_OK;
-}
+static int grow(double **p, size_t *cap, size_t need) { return grow_dev((void **)p, cap, need); }
 
 static void free_handle(rvk_handle *h) {
     if (!h) return;
@@ -721,6 +742,8 @@ static void free_handle(rvk_handle *h) {
     (void)hipFree(h->d_inst);
     (void)hipFree(h->d_theta);
     (void)hipFree(h->d_out);
+    (void)hipFree(h->d_tq);
+    (void)hipFree(h->d_iq);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -822,7 +845,6 @@ int rvk_sync(rvk_handle *h) {
 static int check_rows(rvk_handle *h, int64_t W, int64_t stride) {
     if (!h) return fail(RVK_E_ARG, "NULL handle");
     if (W < 0) return fail(RVK_E_ARG, "negative row count");
-    if (W < 0) return fail(RVK_E_ARG, "n_walkers < 0");
     long long pfull = 5LL * h->n_planets + 2LL * h->n_inst + 2;
     if (stride < pfull) return fail(RVK_E_ARG, "row_stride < P_full = 5*n_planets + 2*n_inst + 2");
     return RVK_OK;
@@ -858,9 +880,12 @@ int rvk_loglike(rvk_handle *h, const double *theta, int64_t W, int64_t stride, d
     size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
     if ((rc = grow(&h->d_theta, &h->cap_theta, bt))) return rc;
     if ((rc = grow(&h->d_out, &h->cap_out, bo))) return rc;
-    HIPCHK(hipMemcpyAsync(h->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
-    if ((rc = rvk_loglike_device(h, h->d_theta, W, stride, h->d_out, h->stream))) return rc;
-    HIPCHK(hipMemcpyAsync(out, h->d_out, bo, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(h->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_loglike_device(h, h->d_theta, W, stride, h->d_out, h->stream))) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+    }
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, h->d_out, bo, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return RVK_OK;
 }
@@ -906,35 +931,56 @@ int rvk_predict(rvk_handle *h, const double *theta, int64_t S, int64_t stride, c
     if (!theta || !t || !out) return fail(RVK_E_ARG, "NULL host buffer");
     if ((what & RVK_PRED_GAMMA) && h->n_inst > 1 && !inst) return fail(RVK_E_ARG, "inst required for GAMMA");
     HIPCHK(hipSetDevice(h->device));
-    // samples in chunks so the device output block stays <= 2^25 doubles (256 MB)
+    // samples in chunks so the device output block stays <= 2^25 doubles (256 MB); the device
+    // buffers are the handle's (grown on demand, kept across calls, freed by rvk_destroy)
     long long chunk = (1LL << 25) / n_t;
     if (chunk < 1) chunk = 1;
     if (chunk > S) chunk = S;
-    double *d_th = nullptr, *d_t = nullptr, *d_o = nullptr;
-    int32_t *d_i = nullptr;
-    HIPCHK(hipMalloc(&d_th, sizeof(double) * (size_t)chunk * (size_t)stride));
-    HIPCHK(hipMalloc(&d_t, sizeof(double) * n_t));
-    HIPCHK(hipMalloc(&d_o, sizeof(double) * (size_t)chunk * (size_t)n_t));
-    if (inst) {
-        HIPCHK(hipMalloc(&d_i, sizeof(int32_t) * n_t));
-        HIPCHK(hipMemcpyAsync(d_i, inst, sizeof(int32_t) * n_t, hipMemcpyHostToDevice, h->stream));
-    }
-    HIPCHK(hipMemcpyAsync(d_t, t, sizeof(double) * n_t, hipMemcpyHostToDevice, h->stream));
-    for (long long s0 = 0; s0 < S && rc == RVK_OK; s0 += chunk) {
+    if ((rc = grow(&h->d_theta, &h->cap_theta, sizeof(double) * (size_t)chunk * (size_t)stride)) ||
+        (rc = grow(&h->d_out, &h->cap_out, sizeof(double) * (size_t)chunk * (size_t)n_t)) ||
+        (rc = grow(&h->d_tq, &h->cap_tq, sizeof(double) * (size_t)n_t)) ||
+        (inst && (rc = grow_dev((void **)&h->d_iq, &h->cap_iq, sizeof(int32_t) * (size_t)n_t))))
+        return rc;
+    if (inst)
+        HIPCHK_SYNC(h->stream, hipMemcpyAsync(h->d_iq, inst, sizeof(int32_t) * n_t, hipMemcpyHostToDevice, h->stream));
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(h->d_tq, t, sizeof(double) * n_t, hipMemcpyHostToDevice, h->stream));
+    for (long long s0 = 0; s0 < S; s0 += chunk) {
         const long long ns = (S - s0) < chunk ? (S - s0) : chunk;
-        HIPCHK(hipMemcpyAsync(d_th, theta + s0 * stride, sizeof(double) * ns * stride, hipMemcpyHostToDevice,
-                              h->stream));
-        rc = rvk_predict_device(h, d_th, ns, stride, d_t, d_i, n_t, what, d_o, h->stream);
-        if (rc == RVK_OK)
-            HIPCHK(hipMemcpyAsync(out + s0 * n_t, d_o, sizeof(double) * ns * n_t, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK_SYNC(h->stream, hipMemcpyAsync(h->d_theta, theta + s0 * stride, sizeof(double) * ns * stride,
+                                              hipMemcpyHostToDevice, h->stream));
+        if ((rc = rvk_predict_device(h, h->d_theta, ns, stride, h->d_tq, inst ? h->d_iq : nullptr, n_t, what,
+                                     h->d_out, h->stream))) {
+            (void)hipStreamSynchronize(h->stream);
+            return rc;
+        }
+        HIPCHK_SYNC(h->stream, hipMemcpyAsync(out + s0 * n_t, h->d_out, sizeof(double) * ns * n_t,
+                                              hipMemcpyDeviceToHost, h->stream));
     }
     HIPCHK(hipStreamSynchronize(h->stream));
-    (void)hipFree(d_th);
-    (void)hipFree(d_t);
-    (void)hipFree(d_o);
-    (void)hipFree(d_i);
-    return rc;
+    return RVK_OK;
 }
+
+}  // extern "C"
+
+namespace {
+// Owns a device allocation for the length of one call (freed on every return path).
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() { (void)hipFree(p); }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+struct OwnedStream {
+    hipStream_t s = nullptr;
+    ~OwnedStream() {
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    }
+};
+}  // namespace
+
+extern "C" {
 
 int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, double *sinE, int32_t device,
                      int32_t solver) {
@@ -945,30 +991,31 @@ int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, 
     int rc = check_gfx950(device);
     if (rc) return rc;
     HIPCHK(hipSetDevice(device));
-    double *dM, *de, *dc, *ds;
-    SC *dtab;
-    if ((rc = upload_table(&dtab))) return rc;
-    size_t b = sizeof(double) * (size_t)n;
-    HIPCHK(hipMalloc(&dM, b));
-    HIPCHK(hipMalloc(&de, b));
-    HIPCHK(hipMalloc(&dc, b));
-    HIPCHK(hipMalloc(&ds, b));
-    HIPCHK(hipMemcpy(dM, M, b, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(de, e, b, hipMemcpyHostToDevice));
+    const SC *dtab = nullptr;
+    if ((rc = shared_table(device, &dtab))) return rc;
+    // RAII: every buffer and the call's own stream are released on every return path (the
+    // stream is drained first, so no copy into the caller's arrays is left in flight)
+    DevBuf dM, de, dc, ds;
+    OwnedStream st;
+    const size_t b = sizeof(double) * (size_t)n;
+    HIPCHK(hipMalloc(&dM.p, b));
+    HIPCHK(hipMalloc(&de.p, b));
+    HIPCHK(hipMalloc(&dc.p, b));
+    HIPCHK(hipMalloc(&ds.p, b));
+    HIPCHK(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
+    HIPCHK(hipMemcpyAsync(dM.p, M, b, hipMemcpyHostToDevice, st.s));
+    HIPCHK(hipMemcpyAsync(de.p, e, b, hipMemcpyHostToDevice, st.s));
+    const dim3 grid((unsigned)((n + 255) / 256));
     if (solver == 1)
-        hipLaunchKernelGGL(kepler_kernel<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dM, de, (long long)n,
-                           dtab, dc, ds);
+        hipLaunchKernelGGL(kepler_kernel<1>, grid, dim3(256), 0, st.s, dM.as<double>(), de.as<double>(), (long long)n,
+                           dtab, dc.as<double>(), ds.as<double>());
     else
-        hipLaunchKernelGGL(kepler_kernel<0>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dM, de, (long long)n,
-                           dtab, dc, ds);
+        hipLaunchKernelGGL(kepler_kernel<0>, grid, dim3(256), 0, st.s, dM.as<double>(), de.as<double>(), (long long)n,
+                           dtab, dc.as<double>(), ds.as<double>());
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(cosE, dc, b, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(sinE, ds, b, hipMemcpyDeviceToHost));
-    (void)hipFree(dM);
-    (void)hipFree(de);
-    (void)hipFree(dc);
-    (void)hipFree(ds);
-    (void)hipFree(dtab);
+    HIPCHK(hipMemcpyAsync(cosE, dc.p, b, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipMemcpyAsync(sinE, ds.p, b, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
     return RVK_OK;
 }
 

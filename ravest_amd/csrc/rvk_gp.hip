@@ -613,15 +613,7 @@ struct rvk_gp {
     size_t cap_theta = 0, cap_hyper = 0, cap_out = 0;
 };
 
-static int gp_grow(double **p, size_t *cap, size_t need) {
-    if (need <= *cap) return RVK_OK;
-    if (*p) HIPCHK(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    HIPCHK(hipMalloc(p, need));
-    *cap = need;
-    return RVK_OK;
-}
+static int gp_grow(double **p, size_t *cap, size_t need) { return grow_dev((void **)p, cap, need); }
 
 static void free_gp(rvk_gp *g) {
     if (!g) return;
@@ -714,10 +706,13 @@ int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t 
     if ((rc = gp_grow(&g->d_theta, &g->cap_theta, bt)) || (rc = gp_grow(&g->d_hyper, &g->cap_hyper, bh)) ||
         (rc = gp_grow(&g->d_out, &g->cap_out, sizeof(double) * (size_t)W)))
         return rc;
-    HIPCHK(hipMemcpyAsync(g->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(g->d_hyper, hyper, bh, hipMemcpyHostToDevice, h->stream));
-    if ((rc = rvk_gp_loglike_device(g, g->d_theta, g->d_hyper, W, stride, hstride, g->d_out, h->stream))) return rc;
-    HIPCHK(hipMemcpyAsync(out, g->d_out, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_hyper, hyper, bh, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_gp_loglike_device(g, g->d_theta, g->d_hyper, W, stride, hstride, g->d_out, h->stream))) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+    }
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, g->d_out, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return RVK_OK;
 }

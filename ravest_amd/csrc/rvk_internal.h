@@ -48,7 +48,24 @@ typedef void (*sample_launch_t)(hipStream_t, EpochData, int, int, const double *
 
 int fail(int code, const std::string &msg);
 
+// Grow a device buffer to >= need bytes (contents dropped); the caller owns *p and frees it.
+int grow_dev(void **p, size_t *cap, size_t need);
+
+// Per-device copy of the sin/cos table, uploaded once per process (never freed).
+int shared_table(int device, const SC **tab);
+
 }  // namespace rvk
+
+// As HIPCHK, but first drains `stream`, so no async copy into a caller's buffer is still in
+// flight when the error is returned (the host-buffer entry points).
+#define HIPCHK_SYNC(stream, expr)                                                             \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            (void)hipStreamSynchronize(stream);                                               \
+            return rvk::fail(RVK_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+        }                                                                                     \
+    } while (0)
 
 #define HIPCHK(expr)                                                                          \
     do {                                                                                      \
@@ -65,9 +82,10 @@ struct rvk_handle {
     double *d_t = nullptr, *d_vel = nullptr, *d_s2 = nullptr;
     rvk::SC *d_tab = nullptr;
     int32_t *d_inst = nullptr;
-    // scratch for the host-buffer entry points
-    double *d_theta = nullptr, *d_out = nullptr;
-    size_t cap_theta = 0, cap_out = 0;
+    // scratch for the host-buffer entry points (rvk_loglike, rvk_predict), grown on demand
+    double *d_theta = nullptr, *d_out = nullptr, *d_tq = nullptr;
+    int32_t *d_iq = nullptr;
+    size_t cap_theta = 0, cap_out = 0, cap_tq = 0, cap_iq = 0;
     rvk::loglike_launch_t launch = nullptr;
     rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
     int solver = 0;

@@ -127,6 +127,8 @@ struct rvk_post {
     double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_au = nullptr;
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;              // rvk_stretch_run's per-chunk arguments
+    double *d_xin = nullptr, *d_oin = nullptr;   // rvk_logpost's host-buffer staging, grown on demand
+    size_t cap_xin = 0, cap_oin = 0;
     hipStream_t cap = nullptr;             // capture stream
     hipGraphExec_t graph = nullptr;        // cached kStepsPerGraph-step chunk
     long long graph_H = 0;
@@ -196,6 +198,8 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_au);
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
+    (void)hipFree(p->d_xin);
+    (void)hipFree(p->d_oin);
     if (p->graph) (void)hipGraphExecDestroy(p->graph);
     if (p->cap) (void)hipStreamDestroy(p->cap);
     delete p;
@@ -321,24 +325,18 @@ int rvk_logpost(rvk_post *p, const double *xf, int64_t W, int64_t stride, double
     if (!xf || !out) return fail(RVK_E_ARG, "NULL host buffer");
     rvk_handle *h = p->h;
     HIPCHK(hipSetDevice(h->device));
-    double *d_x = nullptr, *d_o = nullptr;
-    HIPCHK(hipMalloc(&d_x, sizeof(double) * (size_t)W * (size_t)stride));
-    if (hipMalloc(&d_o, sizeof(double) * (size_t)W) != hipSuccess) {
-        (void)hipFree(d_x);
-        return fail(RVK_E_HIP, "hipMalloc failed");
+    const size_t bx = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
+    int rc;
+    if ((rc = grow_dev((void **)&p->d_xin, &p->cap_xin, bx)) || (rc = grow_dev((void **)&p->d_oin, &p->cap_oin, bo)))
+        return rc;
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(p->d_xin, xf, bx, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_logpost_device(p, p->d_xin, W, stride, p->d_oin, h->stream))) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
     }
-    int rc = RVK_OK;
-    if (hipMemcpyAsync(d_x, xf, sizeof(double) * (size_t)W * (size_t)stride, hipMemcpyHostToDevice, h->stream) !=
-        hipSuccess)
-        rc = fail(RVK_E_HIP, "hipMemcpyAsync H2D failed");
-    if (rc == RVK_OK) rc = rvk_logpost_device(p, d_x, W, stride, d_o, h->stream);
-    if (rc == RVK_OK &&
-        hipMemcpyAsync(out, d_o, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-        rc = fail(RVK_E_HIP, "hipMemcpyAsync D2H failed");
-    if (hipStreamSynchronize(h->stream) != hipSuccess && rc == RVK_OK) rc = fail(RVK_E_HIP, "stream sync failed");
-    (void)hipFree(d_x);
-    (void)hipFree(d_o);
-    return rc;
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, p->d_oin, bo, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RVK_OK;
 }
 
 int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n_steps, double a, uint64_t seed,

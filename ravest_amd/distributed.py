@@ -88,9 +88,10 @@ class ShardedDevicePosterior:
         self.evaluate = evaluate
         self.group = group
         self.dist = dist
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self._inplace = dist.get_backend(group) == "nccl"   # RCCL's in-place all-gather (send = recv + r*n)
+        init = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if init else 1      # no process group: one GPU
+        self.rank = dist.get_rank(group) if init else 0
+        self._inplace = init and dist.get_backend(group) == "nccl"   # RCCL's in-place all-gather
         self._bufs = {}
 
     def bounds(self, n: int):
