@@ -13,10 +13,20 @@
  *            (tinygp 0.3 GaussianProcess(kernel, X=t, diag=...).log_probability(r),
  *             DirectSolver: Cholesky; tinygp is not in this image -- its published
  *             algorithm is restated, see DESIGN.md "GP").
- * Factorisation in fp32 (BASELINE config 5 is fp32), mean model and the
- * final sums in fp64.  An invalid planet gives -inf (the reference's mean-model
- * fail-fast); a covariance that is not positive definite in fp32 gives NaN.
- * Epochs: 1 <= n_epochs <= 1024.
+ * Mean model and the final sums in fp64; the factorisation in the handle's
+ * precision mode (rvk_gp_set_precision):
+ *   RVK_GP_FP32                fp32 blocked Cholesky on MFMA (BASELINE config 5 is
+ *                              fp32); a covariance that is not positive definite in
+ *                              fp32 gives NaN;
+ *   RVK_GP_FP32_FP64_FALLBACK  (default) as RVK_GP_FP32, then every walker the fp32
+ *                              factorisation rejected (NaN) is re-evaluated in fp64 in
+ *                              the same stream-ordered call -- no host round trip;
+ *   RVK_GP_FP64                fp64 throughout (the reference's precision: ravest runs
+ *                              tinygp with jax_enable_x64, fit.py:39); NaN only where
+ *                              the covariance is not positive definite in fp64.
+ * An invalid planet gives -inf (the reference's mean-model fail-fast).
+ * Epochs: 1 <= n_epochs <= 1024.  Calls on one rvk_gp share its workspaces: keep
+ * them on one stream (or serialise them).
  *
  * hyper row layout [W][hyper_stride] fp64: gp_amp, gp_lambda_e, gp_lambda_p,
  * gp_period (GPKernel.expected_hyperparams order, gp.py:37).
@@ -27,6 +37,7 @@
 #include <stdint.h>
 
 #include "rvk.h"
+#include "rvk_post.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -36,7 +47,12 @@ extern "C" {
 #define RVK_GP_NHYPER        4
 #define RVK_GP_MAX_EPOCHS    1024
 
+#define RVK_GP_FP32                 0
+#define RVK_GP_FP32_FP64_FALLBACK   1
+#define RVK_GP_FP64                 2
+
 typedef struct rvk_gp rvk_gp;
+typedef struct rvk_gp_post rvk_gp_post;
 
 /* GP likelihood over the handle's dataset, planets and parameterisation.  The
  * handle must outlive it. */
@@ -50,6 +66,45 @@ int rvk_gp_loglike_device(rvk_gp *g, const double *d_theta, const double *d_hype
 /* Host buffers, blocking. */
 int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t n_walkers,
                    int64_t row_stride, int64_t hyper_stride, double *out);
+
+/* Precision mode of the factorisation (RVK_GP_FP32 / _FP32_FP64_FALLBACK / _FP64). */
+int rvk_gp_set_precision(rvk_gp *g, int32_t mode);
+
+/* GP-conditioned posterior predictive (GPFitter.calculate_rv_gp_custom, fit.py:7494-7554,
+ * and calculate_rv_gp_from_samples, fit.py:7342-7386), fp64: for every sample s (a theta
+ * row and a hyper row), the GP conditioned on the residuals r = vel - mean(t_data) with
+ * the diagonal velerr^2 + jit^2, evaluated at the query times:
+ *   out[s][q] = K(t_q, t_data) (K(t_data, t_data) + diag)^-1 r
+ * (tinygp GaussianProcess.condition(y, X_test).mean, zero mean function).  A sample
+ * with an invalid planet gives a row of NaN (the reference's Planet() raises). */
+int rvk_gp_predict_device(rvk_gp *g, const double *d_theta, const double *d_hyper, int64_t n_samples,
+                          int64_t row_stride, int64_t hyper_stride, const double *d_tq, int64_t n_times,
+                          double *d_out, void *stream);
+int rvk_gp_predict(rvk_gp *g, const double *theta, const double *hyper, int64_t n_samples,
+                   int64_t row_stride, int64_t hyper_stride, const double *tq, int64_t n_times,
+                   double *out);
+
+/* GP log-posterior (GPLogPosterior, fit.py:7596-7939), batched over walkers.
+ * The walker's combined row is [theta_full (rvk.h layout) | gp_amp, gp_lambda_e,
+ * gp_lambda_p, gp_period] (P_full + 4 columns); free_idx[n_free] gives the combined-row
+ * column of each free coordinate, in emcee's order (free_params_names then
+ * free_hyperparams_names, fit.py:4982); template_row[P_full + 4] holds the fixed values.
+ * Prior slots (include/rvk_post.h kinds and sources; sources index the combined row)
+ * [0, n_param_prior) are the LogPrior over the parameters and [n_param_prior, n_prior)
+ * the hyperpriors, each summed in the given (the reference's dict) order.
+ * out = (((ll + lp) + lhp) + log_jacobian) + log_renorm; -inf for a negative jitter,
+ * invalid hyperparameters (non-finite or <= 0, gp.py:73-82), a prior-side conversion
+ * error, a non-finite log-prior or log-hyperprior, or an invalid planet -- the
+ * reference's order of checks (fit.py:7849-7901).  The GP handle must outlive it. */
+rvk_gp_post *rvk_gp_post_create(rvk_gp *g, int32_t n_free, const int32_t *free_idx, const double *template_row,
+                                int32_t n_prior, int32_t n_param_prior, const int32_t *prior_kind,
+                                const int32_t *prior_src, const double *prior_par, double log_jacobian,
+                                double log_renorm, int32_t flags);
+void rvk_gp_post_destroy(rvk_gp_post *p);
+int rvk_gp_post_reserve(rvk_gp_post *p, int64_t max_walkers);
+int rvk_gp_logpost_device(rvk_gp_post *p, const double *d_free, int64_t n_walkers, int64_t row_stride,
+                          double *d_out, void *stream);
+int rvk_gp_logpost(rvk_gp_post *p, const double *free, int64_t n_walkers, int64_t row_stride, double *out);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,9 @@ EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rv
            "rvk_last_error", "rvk_version",
            "rvk_post_create", "rvk_post_destroy", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
            "rvk_stretch_run",
-           "rvk_gp_create", "rvk_gp_destroy", "rvk_gp_loglike", "rvk_gp_loglike_device"]
+           "rvk_gp_create", "rvk_gp_destroy", "rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_gp_set_precision",
+           "rvk_gp_predict", "rvk_gp_predict_device", "rvk_gp_post_create", "rvk_gp_post_destroy",
+           "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device"]
 
 OPT_SOLVER = 1
 OPT_GRAPH = 2
@@ -39,6 +41,8 @@ PRIOR_KIND = {"Uniform": 0, "EccentricityUniform": 1, "Normal": 2, "TruncatedNor
 POST_CONVERT = 1
 GP_QUASIPERIODIC = 0
 GP_NHYPER = 4
+# include/rvk_gp.h precision modes
+GP_FP32, GP_FP32_FP64_FALLBACK, GP_FP64 = 0, 1, 2
 
 
 def prior_src_default(planet: int, j: int) -> int:
@@ -99,7 +103,19 @@ def load() -> C.CDLL:
     L.rvk_gp_destroy.restype = None
     L.rvk_gp_loglike.argtypes = [vp, dp, dp, C.c_int64, C.c_int64, C.c_int64, dp]
     L.rvk_gp_loglike_device.argtypes = [vp, vp, vp, C.c_int64, C.c_int64, C.c_int64, vp, vp]
-    for name in ("rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
+    L.rvk_gp_set_precision.argtypes = [vp, C.c_int32]
+    L.rvk_gp_predict.argtypes = [vp, dp, dp, C.c_int64, C.c_int64, C.c_int64, dp, C.c_int64, dp]
+    L.rvk_gp_predict_device.argtypes = [vp, vp, vp, C.c_int64, C.c_int64, C.c_int64, vp, C.c_int64, vp, vp]
+    L.rvk_gp_post_create.argtypes = [vp, C.c_int32, ip, dp, C.c_int32, C.c_int32, ip, ip, dp, C.c_double,
+                                     C.c_double, C.c_int32]
+    L.rvk_gp_post_create.restype = vp
+    L.rvk_gp_post_destroy.argtypes = [vp]
+    L.rvk_gp_post_destroy.restype = None
+    L.rvk_gp_post_reserve.argtypes = [vp, C.c_int64]
+    L.rvk_gp_logpost.argtypes = [vp, dp, C.c_int64, C.c_int64, dp]
+    L.rvk_gp_logpost_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
+    for name in ("rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_gp_set_precision", "rvk_gp_predict",
+                 "rvk_gp_predict_device", "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device", "rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
                  "rvk_set_option", "rvk_reserve", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
                  "rvk_stretch_run"):
         getattr(L, name).restype = C.c_int

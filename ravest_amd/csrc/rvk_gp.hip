@@ -30,11 +30,12 @@
 // Padding rows/columns up to a multiple of 32 are identity rows with r = 0.
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
 #include "../../include/rvk_gp.h"
-#include "rvk_internal.h"
+#include "rvk_gp_internal.h"
 
 using namespace rvk;
 
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                                                                              const short *__restrict__ slots,
                                                                              float *__restrict__ work,
                                                                              long long work_stride,
-                                                                             double *__restrict__ out) {
+                                                                             double *__restrict__ out, GpPost post) {
     constexpr int NT = 64 * NW;
     extern __shared__ double smem_d[];
     const int nt = (n + TB - 1) / TB, npad = nt * TB;
@@ -167,6 +168,10 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
     float *A = work + (long long)blockIdx.x * work_stride;
 
     for (long long w = blockIdx.x; w < W; w += gridDim.x) {
+        if (post.lp && post.lp[w] == -INFINITY) {        // rejected before the likelihood (uniform)
+            if (tid == 0) out[w] = -INFINITY;
+            continue;
+        }
         const double *row = theta + w * stride;
         const double *hp = hyper + w * hstride;
         // ---- 1. planets, mean model, residuals -------------------------------------------
@@ -513,8 +518,10 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 qs += L.red[3 * u];
                 ls += L.red[3 * u + 1];
             }
-            const double ll = -0.5 * qs - 0.5 * ls - 0.5 * (double)n * kLog2Pi;
-            out[w] = __builtin_isfinite(ll) ? ll : NAN;     // not positive definite in fp32: NaN
+            double ll = -0.5 * qs - 0.5 * ls - 0.5 * (double)n * kLog2Pi;
+            if (!__builtin_isfinite(ll)) ll = NAN;          // not positive definite in fp32: NaN
+            if (post.lp) ll = (((ll + post.lp[w]) + post.lhp[w]) + post.jac) + post.renorm;
+            out[w] = ll;
         }
         __syncthreads();
     }
@@ -570,12 +577,12 @@ GpShape gp_shape(int n, int prefer_nw) {
 
 typedef void (*gp_launch_t)(hipStream_t, unsigned, size_t, EpochData, int, int, int, const double *,
                             const double *, long long, long long, long long, const short *, float *, long long,
-                            double *);
+                            double *, GpPost);
 
 template <bool MULTI, bool TP, int NW, int MAXR>
 void launch_gp(hipStream_t st, unsigned grid, size_t lds, EpochData d, int n, int ni, int np, const double *th,
                const double *hy, long long W, long long stride, long long hs, const short *slots, float *work,
-               long long wstride, double *out) {
+               long long wstride, double *out, GpPost post) {
     static size_t allowed = 0;   // dynamic LDS beyond the default needs the attribute
     if (lds > allowed) {
         (void)hipFuncSetAttribute((const void *)gp_loglike_kernel<MULTI, TP, NW, MAXR>,
@@ -583,7 +590,7 @@ void launch_gp(hipStream_t st, unsigned grid, size_t lds, EpochData d, int n, in
         allowed = lds;
     }
     hipLaunchKernelGGL((gp_loglike_kernel<MULTI, TP, NW, MAXR>), dim3(grid), dim3(64 * NW), lds, st, d, n, ni, np,
-                       th, hy, W, stride, hs, slots, work, wstride, out);
+                       th, hy, W, stride, hs, slots, work, wstride, out, post);
 }
 
 template <int NW, int MAXR>
@@ -598,19 +605,86 @@ gp_launch_t pick_gp(int np, bool multi, bool tp, GpShape sh) {
     return sh.maxr == 2 ? pick_gp_w<8, 2>(multi, tp) : pick_gp_w<8, 4>(multi, tp);
 }
 
+// GP log-prior of a walker block (GPLogPosterior.log_probability up to the likelihood,
+// fit.py:7851-7885), one wave per walker: the combined row [theta_full | hyper] from the
+// fixed template and the free coordinates, the jitter check, the hyperparameter validity
+// (GPKernel._validate_hyperparams_values: finite and > 0, gp.py:73-82), the prior-side
+// conversion, the prior terms; priors (slots [0, n_lp)) and hyperpriors (the rest) are
+// summed separately, each in the reference's key order.  lp = -inf rejects the walker.
+__global__ __launch_bounds__(256) void gp_logprior_kernel(PostDev pd, int n_lp, const double *__restrict__ xf,
+                                                          long long W, long long stride, double *__restrict__ full,
+                                                          double *__restrict__ lp, double *__restrict__ lhp) {
+    __shared__ PostWaveLds lds[kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    PostWaveLds &L = lds[wv];
+    const int hy0 = pd.p_full - RVK_GP_NHYPER;            // first hyperparameter column
+    for (long long w = (long long)blockIdx.x * kWavesPerBlock + wv; w < W; w += (long long)gridDim.x * kWavesPerBlock) {
+        for (int c = lane; c < pd.n_free; c += 64) L.x[c] = xf[w * stride + c];
+        wave_lds_sync();
+        double *frow = full + w * pd.p_full;
+        for (int c = lane; c < pd.p_full; c += 64) {
+            const int f = pd.colmap[c];
+            const double v = f >= 0 ? L.x[f] : pd.tmpl[c];
+            L.f[c] = v;
+            frow[c] = v;
+        }
+        wave_lds_sync();
+        const int jit0 = 5 * pd.n_planets + pd.n_inst;
+        bool dead = false;
+        if (lane < pd.n_inst) dead = L.f[jit0 + lane] < 0.0;                          // fit.py:7853-7856
+        if (lane < RVK_GP_NHYPER) {                                                     // fit.py:7860-7867
+            const double v = L.f[hy0 + lane];
+            dead |= !(__builtin_isfinite(v) && v > 0.0);
+        }
+        if (pd.convert && lane < pd.n_planets) {                                        // fit.py:7787-7834
+            double *dp = L.def + 5 * lane;
+            dead |= !to_default_t<-1>(L.f + 5 * lane, dp[0], dp[1], dp[2], dp[3], dp[4], pd.par);
+        }
+        wave_lds_sync();
+        for (int k = lane; k < pd.n_prior; k += 64) {
+            const PriorSlot &sl = pd.slots[k];
+            const double v = sl.src >= 0 ? L.f[sl.src] : L.def[-sl.src - 1];
+            L.term[k] = prior_lp(sl, v);
+        }
+        wave_lds_sync();
+        dead = __builtin_amdgcn_ballot_w64(dead) != 0;
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < n_lp; ++k) a += L.term[k];                                  // LogPrior, dict order
+        for (int k = n_lp; k < pd.n_prior; ++k) b += L.term[k];                         // hyperpriors
+        if (!__builtin_isfinite(a) || !__builtin_isfinite(b)) dead = true;              // fit.py:7878-7885
+        if (lane == 0) {
+            lp[w] = dead ? -INFINITY : a;
+            lhp[w] = b;
+        }
+        wave_lds_sync();
+    }
+}
+
+unsigned gp_wave_blocks(long long n) {
+    long long b = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
+}
+
 }  // namespace
 
 struct rvk_gp {
     rvk_handle *h = nullptr;
+    int mode = RVK_GP_FP32_FP64_FALLBACK;
     gp_launch_t launch = nullptr;
     unsigned grid = 0;           // concurrent walkers (one workgroup each)
     size_t lds = 0;
     long long wstride = 0;       // floats per workgroup workspace
     float *d_work = nullptr;
     short *d_slots = nullptr;    // [nt][nt] tile -> workspace slot
-    // host-buffer path (rvk_gp_loglike): device copies kept across calls, grown on demand
-    double *d_theta = nullptr, *d_hyper = nullptr, *d_out = nullptr;
-    size_t cap_theta = 0, cap_hyper = 0, cap_out = 0;
+    // fp64 factorisation / conditioning (rvk_gp64.hip)
+    gp64_launch_t launch64 = nullptr, cond64 = nullptr;
+    unsigned grid64 = 0;
+    size_t lds64 = 0;
+    long long w64stride = 0;     // doubles per workgroup workspace
+    double *d_work64 = nullptr;
+    // host-buffer paths (rvk_gp_loglike, rvk_gp_predict): device copies kept across calls, grown on demand
+    double *d_theta = nullptr, *d_hyper = nullptr, *d_out = nullptr, *d_tq = nullptr;
+    size_t cap_theta = 0, cap_hyper = 0, cap_out = 0, cap_tq = 0;
 };
 
 static int gp_grow(double **p, size_t *cap, size_t need) { return grow_dev((void **)p, cap, need); }
@@ -620,9 +694,11 @@ static void free_gp(rvk_gp *g) {
     if (g->h) (void)hipSetDevice(g->h->device);
     (void)hipFree(g->d_work);
     (void)hipFree(g->d_slots);
+    (void)hipFree(g->d_work64);
     (void)hipFree(g->d_theta);
     (void)hipFree(g->d_hyper);
     (void)hipFree(g->d_out);
+    (void)hipFree(g->d_tq);
     delete g;
 }
 
@@ -652,6 +728,54 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     HIPCHK(hipMalloc(&g->d_work, sizeof(float) * (size_t)g->wstride * g->grid));
     HIPCHK(hipMalloc(&g->d_slots, sizeof(short) * slots.size()));
     HIPCHK(hipMemcpy(g->d_slots, slots.data(), sizeof(short) * slots.size(), hipMemcpyHostToDevice));
+    // fp64 path: one 4-wave-per-SIMD workgroup per CU, the whole lower triangle of L per workgroup
+    const Gp64Shape s64 = gp64_shape(h->n);
+    g->launch64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, false, s64);
+    g->cond64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, true, s64);
+    g->lds64 = gp64_lds_bytes(h->n, s64.nw);
+    g->grid64 = (unsigned)prop.multiProcessorCount;
+    g->w64stride = gp64_work_doubles(h->n);
+    HIPCHK(hipMalloc(&g->d_work64, sizeof(double) * (size_t)g->w64stride * g->grid64));
+    return RVK_OK;
+}
+
+static Gp64Args args64(rvk_gp *g, const double *th, const double *hy, long long W, long long stride, long long hs) {
+    rvk_handle *h = g->h;
+    Gp64Args a{};
+    a.d = h->epochs();
+    a.n = h->n;
+    a.ni = h->n_inst;
+    a.np = h->n_planets;
+    a.theta = th;
+    a.hyper = hy;
+    a.W = W;
+    a.stride = stride;
+    a.hstride = hs;
+    a.work = g->d_work64;
+    a.work_stride = g->w64stride;
+    return a;
+}
+
+// The GP log-likelihood (or log-posterior, post.lp set) of a device walker block, in the
+// handle's precision mode; stream-ordered.
+static int gp_run(rvk_gp *g, const double *th, const double *hy, long long W, long long stride, long long hs,
+                  double *out, GpPost post, hipStream_t st) {
+    rvk_handle *h = g->h;
+    if (g->mode != RVK_GP_FP64) {
+        const unsigned grid = (unsigned)((long long)g->grid < W ? g->grid : W);
+        g->launch(st, grid, g->lds, h->epochs(), h->n, h->n_inst, h->n_planets, th, hy, W, stride, hs, g->d_slots,
+                  g->d_work, g->wstride, out, post);
+        HIPCHK(hipGetLastError());
+    }
+    if (g->mode != RVK_GP_FP32) {
+        Gp64Args a = args64(g, th, hy, W, stride, hs);
+        a.out = out;
+        a.post = post;
+        a.gate = g->mode == RVK_GP_FP64 ? nullptr : out;   // fallback: the fp32 NaN walkers only
+        const unsigned grid = (unsigned)((long long)g->grid64 < W ? g->grid64 : W);
+        g->launch64(st, grid, g->lds64, a);
+        HIPCHK(hipGetLastError());
+    }
     return RVK_OK;
 }
 
@@ -678,6 +802,14 @@ rvk_gp *rvk_gp_create(rvk_handle *h, int32_t kernel_type) {
 
 void rvk_gp_destroy(rvk_gp *g) { free_gp(g); }
 
+int rvk_gp_set_precision(rvk_gp *g, int32_t mode) {
+    if (!g) return fail(RVK_E_ARG, "NULL GP handle");
+    if (mode != RVK_GP_FP32 && mode != RVK_GP_FP32_FP64_FALLBACK && mode != RVK_GP_FP64)
+        return fail(RVK_E_ARG, "unknown GP precision mode");
+    g->mode = mode;
+    return RVK_OK;
+}
+
 int rvk_gp_loglike_device(rvk_gp *g, const double *d_theta, const double *d_hyper, int64_t W, int64_t stride,
                           int64_t hstride, double *d_out, void *stream) {
     if (!g) return fail(RVK_E_ARG, "NULL GP handle");
@@ -686,11 +818,8 @@ int rvk_gp_loglike_device(rvk_gp *g, const double *d_theta, const double *d_hype
     if (W == 0) return RVK_OK;
     if (!d_theta || !d_hyper || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     HIPCHK(hipSetDevice(h->device));
-    const unsigned grid = (unsigned)((long long)g->grid < W ? g->grid : W);
-    g->launch((hipStream_t)stream, grid, g->lds, h->epochs(), h->n, h->n_inst, h->n_planets, d_theta, d_hyper, W, stride,
-              hstride, g->d_slots, g->d_work, g->wstride, d_out);
-    HIPCHK(hipGetLastError());
-    return RVK_OK;
+    return gp_run(g, d_theta, d_hyper, W, stride, hstride, d_out, GpPost{nullptr, nullptr, 0.0, 0.0},
+                  (hipStream_t)stream);
 }
 
 int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t W, int64_t stride, int64_t hstride,
@@ -713,6 +842,213 @@ int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t 
         return rc;
     }
     HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, g->d_out, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RVK_OK;
+}
+
+int rvk_gp_predict_device(rvk_gp *g, const double *d_theta, const double *d_hyper, int64_t S, int64_t stride,
+                          int64_t hstride, const double *d_tq, int64_t T, double *d_out, void *stream) {
+    if (!g) return fail(RVK_E_ARG, "NULL GP handle");
+    rvk_handle *h = g->h;
+    if (S < 0 || T < 0 || stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad sample block shape");
+    if (S == 0 || T == 0) return RVK_OK;
+    if (!d_theta || !d_hyper || !d_tq || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
+    HIPCHK(hipSetDevice(h->device));
+    Gp64Args a = args64(g, d_theta, d_hyper, S, stride, hstride);
+    a.tq = d_tq;
+    a.T = T;
+    a.pred = d_out;
+    const unsigned grid = (unsigned)((long long)g->grid64 < S ? g->grid64 : S);
+    g->cond64((hipStream_t)stream, grid, g->lds64, a);
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_gp_predict(rvk_gp *g, const double *theta, const double *hyper, int64_t S, int64_t stride, int64_t hstride,
+                   const double *tq, int64_t T, double *out) {
+    if (!g) return fail(RVK_E_ARG, "NULL GP handle");
+    if (S == 0 || T == 0) return RVK_OK;
+    if (!theta || !hyper || !tq || !out || S < 0 || T < 0) return fail(RVK_E_ARG, "bad host buffers");
+    rvk_handle *h = g->h;
+    if (stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad sample block shape");
+    HIPCHK(hipSetDevice(h->device));
+    const size_t bt = sizeof(double) * (size_t)S * (size_t)stride, bh = sizeof(double) * (size_t)S * (size_t)hstride;
+    const size_t bq = sizeof(double) * (size_t)T, bo = sizeof(double) * (size_t)S * (size_t)T;
+    int rc;
+    if ((rc = gp_grow(&g->d_theta, &g->cap_theta, bt)) || (rc = gp_grow(&g->d_hyper, &g->cap_hyper, bh)) ||
+        (rc = gp_grow(&g->d_tq, &g->cap_tq, bq)) || (rc = gp_grow(&g->d_out, &g->cap_out, bo)))
+        return rc;
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_hyper, hyper, bh, hipMemcpyHostToDevice, h->stream));
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_tq, tq, bq, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_gp_predict_device(g, g->d_theta, g->d_hyper, S, stride, hstride, g->d_tq, T, g->d_out, h->stream))) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+    }
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, g->d_out, bo, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RVK_OK;
+}
+
+}  // extern "C"
+
+// ---- GP log-posterior ---------------------------------------------------------------------
+
+struct rvk_gp_post {
+    rvk_gp *g = nullptr;
+    int n_free = 0, n_prior = 0, n_lp = 0, p_comb = 0;
+    bool convert = false;
+    double jac = 0.0, renorm = 0.0;
+    int32_t *d_colmap = nullptr;
+    double *d_tmpl = nullptr;
+    PriorSlot *d_slots = nullptr;
+    long long capw = 0;
+    double *d_full = nullptr, *d_lp = nullptr, *d_lhp = nullptr;   // workspace for capw walkers
+    double *d_xin = nullptr, *d_oin = nullptr;                     // rvk_gp_logpost's staging
+    size_t cap_xin = 0, cap_oin = 0;
+
+    PostDev dev() const {
+        const rvk_handle *h = g->h;
+        return PostDev{n_free, p_comb, n_prior, h->n_planets, h->n_inst, h->par, convert, d_colmap, d_tmpl, d_slots};
+    }
+};
+
+static void free_gp_post(rvk_gp_post *p) {
+    if (!p) return;
+    if (p->g) (void)hipSetDevice(p->g->h->device);
+    (void)hipFree(p->d_colmap);
+    (void)hipFree(p->d_tmpl);
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_full);
+    (void)hipFree(p->d_lp);
+    (void)hipFree(p->d_lhp);
+    (void)hipFree(p->d_xin);
+    (void)hipFree(p->d_oin);
+    delete p;
+}
+
+static int gp_post_reserve(rvk_gp_post *p, long long W) {
+    if (W <= p->capw) return RVK_OK;
+    HIPCHK(hipSetDevice(p->g->h->device));
+    (void)hipFree(p->d_full);
+    (void)hipFree(p->d_lp);
+    (void)hipFree(p->d_lhp);
+    p->d_full = p->d_lp = p->d_lhp = nullptr;
+    p->capw = 0;
+    HIPCHK(hipMalloc(&p->d_full, sizeof(double) * (size_t)W * (size_t)p->p_comb));
+    HIPCHK(hipMalloc(&p->d_lp, sizeof(double) * (size_t)W));
+    HIPCHK(hipMalloc(&p->d_lhp, sizeof(double) * (size_t)W));
+    p->capw = W;
+    return RVK_OK;
+}
+
+static int create_gp_post(rvk_gp_post *p, rvk_gp *g, int32_t n_free, const int32_t *free_idx, const double *tmpl,
+                          int32_t n_prior, int32_t n_param_prior, const int32_t *kind, const int32_t *src,
+                          const double *par, double jac, double renorm, int32_t flags) {
+    if (!g) return fail(RVK_E_ARG, "NULL GP handle");
+    rvk_handle *h = g->h;
+    const int pc = h->p_full() + RVK_GP_NHYPER;
+    if (n_free < 1 || n_free > pc || !free_idx || !tmpl) return fail(RVK_E_ARG, "bad free-parameter layout");
+    if (n_prior < 0 || n_param_prior < 0 || n_param_prior > n_prior || (n_prior > 0 && (!kind || !src || !par)))
+        return fail(RVK_E_ARG, "bad prior arrays");
+    if (flags & ~RVK_POST_CONVERT) return fail(RVK_E_ARG, "unknown flags");
+    std::vector<int32_t> colmap(pc, -1);
+    for (int i = 0; i < n_free; ++i) {
+        if (free_idx[i] < 0 || free_idx[i] >= pc) return fail(RVK_E_ARG, "free_idx out of range");
+        if (colmap[free_idx[i]] >= 0) return fail(RVK_E_ARG, "free_idx has a duplicate column");
+        colmap[free_idx[i]] = i;
+    }
+    std::vector<PriorSlot> slots(n_prior);
+    bool convert = (flags & RVK_POST_CONVERT) != 0;
+    for (int k = 0; k < n_prior; ++k) {
+        if (kind[k] < RVK_PRIOR_UNIFORM || kind[k] > RVK_PRIOR_BETA) return fail(RVK_E_ARG, "unknown prior kind");
+        if (src[k] >= pc) return fail(RVK_E_ARG, "prior source column out of range");
+        if (src[k] < 0 && -src[k] - 1 >= 5 * h->n_planets) return fail(RVK_E_ARG, "prior source planet out of range");
+        convert |= src[k] < 0;
+        slots[k].kind = kind[k];
+        slots[k].src = src[k];
+        std::memcpy(slots[k].p, par + (size_t)k * RVK_PRIOR_NPAR, sizeof(double) * RVK_PRIOR_NPAR);
+    }
+    p->g = g;
+    p->n_free = n_free;
+    p->n_prior = n_prior;
+    p->n_lp = n_param_prior;
+    p->p_comb = pc;
+    p->convert = convert;
+    p->jac = jac;
+    p->renorm = renorm;
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipMalloc(&p->d_colmap, sizeof(int32_t) * pc));
+    HIPCHK(hipMalloc(&p->d_tmpl, sizeof(double) * pc));
+    HIPCHK(hipMalloc(&p->d_slots, sizeof(PriorSlot) * (n_prior > 0 ? n_prior : 1)));
+    HIPCHK(hipMemcpy(p->d_colmap, colmap.data(), sizeof(int32_t) * pc, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(p->d_tmpl, tmpl, sizeof(double) * pc, hipMemcpyHostToDevice));
+    if (n_prior > 0)
+        HIPCHK(hipMemcpy(p->d_slots, slots.data(), sizeof(PriorSlot) * n_prior, hipMemcpyHostToDevice));
+    return RVK_OK;
+}
+
+extern "C" {
+
+rvk_gp_post *rvk_gp_post_create(rvk_gp *g, int32_t n_free, const int32_t *free_idx, const double *template_row,
+                                int32_t n_prior, int32_t n_param_prior, const int32_t *prior_kind,
+                                const int32_t *prior_src, const double *prior_par, double log_jacobian,
+                                double log_renorm, int32_t flags) {
+    rvk_gp_post *p = new (std::nothrow) rvk_gp_post();
+    if (!p) {
+        fail(RVK_E_NOMEM, "out of host memory");
+        return nullptr;
+    }
+    if (create_gp_post(p, g, n_free, free_idx, template_row, n_prior, n_param_prior, prior_kind, prior_src, prior_par,
+                       log_jacobian, log_renorm, flags)) {
+        free_gp_post(p);
+        return nullptr;
+    }
+    return p;
+}
+
+void rvk_gp_post_destroy(rvk_gp_post *p) { free_gp_post(p); }
+
+int rvk_gp_post_reserve(rvk_gp_post *p, int64_t max_walkers) {
+    if (!p || max_walkers < 0) return fail(RVK_E_ARG, "bad arguments");
+    return gp_post_reserve(p, max_walkers);
+}
+
+int rvk_gp_logpost_device(rvk_gp_post *p, const double *d_free, int64_t W, int64_t stride, double *d_out,
+                          void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL GP posterior");
+    if (W < 0 || stride < p->n_free) return fail(RVK_E_ARG, "bad walker block shape");
+    if (W == 0) return RVK_OK;
+    if (!d_free || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
+    int rc = gp_post_reserve(p, W);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    rvk_handle *h = p->g->h;
+    HIPCHK(hipSetDevice(h->device));
+    hipLaunchKernelGGL(gp_logprior_kernel, dim3(gp_wave_blocks(W)), dim3(256), 0, st, p->dev(), p->n_lp, d_free,
+                       (long long)W, (long long)stride, p->d_full, p->d_lp, p->d_lhp);
+    HIPCHK(hipGetLastError());
+    return gp_run(p->g, p->d_full, p->d_full + h->p_full(), W, p->p_comb, p->p_comb, d_out,
+                  GpPost{p->d_lp, p->d_lhp, p->jac, p->renorm}, st);
+}
+
+int rvk_gp_logpost(rvk_gp_post *p, const double *xf, int64_t W, int64_t stride, double *out) {
+    if (!p) return fail(RVK_E_ARG, "NULL GP posterior");
+    if (W < 0 || stride < p->n_free) return fail(RVK_E_ARG, "bad walker block shape");
+    if (W == 0) return RVK_OK;
+    if (!xf || !out) return fail(RVK_E_ARG, "NULL host buffer");
+    rvk_handle *h = p->g->h;
+    HIPCHK(hipSetDevice(h->device));
+    const size_t bx = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
+    int rc;
+    if ((rc = grow_dev((void **)&p->d_xin, &p->cap_xin, bx)) || (rc = grow_dev((void **)&p->d_oin, &p->cap_oin, bo)))
+        return rc;
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(p->d_xin, xf, bx, hipMemcpyHostToDevice, h->stream));
+    if ((rc = rvk_gp_logpost_device(p, p->d_xin, W, stride, p->d_oin, h->stream))) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+    }
+    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, p->d_oin, bo, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return RVK_OK;
 }

@@ -1,0 +1,568 @@
+// rvk_gp64.hip -- fp64 factorisation of the batched quasi-periodic GP (include/rvk_gp.h):
+// the reference's precision (ravest runs tinygp with jax_enable_x64, fit.py:39), used
+//   * as the RVK_GP_FP64 precision mode of rvk_gp_loglike[_device],
+//   * as the fallback of the fp32 path for walkers whose covariance is not positive
+//     definite in fp32 (gate = the fp32 output: only NaN walkers are re-evaluated),
+//   * for the GP-conditioned posterior predictive (CONDITION mode: tinygp
+//     GaussianProcess.condition(y, X_test).mean, fit.py:7494-7554).
+//
+// One workgroup of NW = 8 waves per walker (one per CU: 2 waves per SIMD, 256 VGPRs each),
+// grid-stride over walkers.  Per walker:
+//   1. planet constants and the fp64 mean model (the log-likelihood kernel's solver) ->
+//      times, residuals r and the diagonal velerr^2 + jit^2 in LDS (fp64);
+//   2. blocked left-looking Cholesky over 32-wide tile columns with the right-hand side
+//      carried along (y = L^-1 r) and a one-column lookahead -- the schedule of the fp32
+//      kernel (rvk_gp.hip), with fp64 tiles as 2 x 2 blocks of v_mfma_f64_16x16x4_f64:
+//        P(k)  the owner of tile row k factors the diagonal tile (one wave: lanes 0-31
+//              the rows of L_kk, lanes 32-63 the columns of X = L_kk^-1, from the same
+//              LDS row broadcasts) and y_k = X r_k; every wave accumulates the next
+//              column's tiles, acc(bi, k+1) = C(bi, k+1) - sum_{j<k} L(bi, j) L(k+1, j)^T;
+//        S1(k) L(bi, k) = acc(bi, k) X^T (MFMA), stored; r_bi -= L(bi, k) y_k;
+//        S2(k) acc(bi, k+1) -= L(bi, k) L(k+1, k)^T, parked in the workspace slot of
+//              tile (bi, k+1) (the diagonal one stays in its owner's registers).
+//      Accumulators hold the NEGATED transposed tiles in MFMA C/D layout (every MFMA
+//      adds; the C/D layout of a transposed tile is the operand layout of the next
+//      product, so tiles are never reshuffled).  Finished tiles are kept in the
+//      walker's workspace in "fragment layout": frag(s, kk)[lane] = T[16 s + (lane & 15)]
+//      [4 kk + (lane >> 4)], which is the A and the B operand layout of the f64 MFMA,
+//      stored as lane-contiguous 16-byte pairs (kk, kk + 1).
+//   3. LOGLIKE: ll = -1/2 y.y - 1/2 sum log L_ii^2 - n/2 log 2 pi (tinygp DirectSolver);
+//      CONDITION: alpha = L^-T y (blocked back substitution over the stored tiles and
+//      diagonal inverses), mean(t_q) = sum_i k(t_q - t_i) alpha_i.
+// The covariance is generated in fp64 from tau = t_i - t_j, as the reference does:
+// A^2 exp(-gamma sin^2(pi |tau| / P) - tau^2 / (2 lambda_e^2))   (gp.py:126-156).
+#include <cmath>
+#include <type_traits>
+
+#include "../../include/rvk_gp.h"
+#include "rvk_gp_internal.h"
+
+using namespace rvk;
+
+namespace {
+
+constexpr int TB = 32;            // tile edge
+constexpr int TILE = TB * TB;     // doubles per tile
+constexpr int FS = 34;            // row stride (doubles) of the factor's row buffer: 16-byte aligned rows
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+
+// Transposed 32 x 32 tile in MFMA f64 C/D layout (cdna_hip_programming.md: 16x16x4 f64 C/D
+// col = lane & 15, row = (lane >> 4) + 4 reg): c[p][q][i] at lane l is element
+// [16 p + (l >> 4) + 4 i][16 q + (l & 15)] of the transposed tile.
+struct Acc {
+    f64x4 c[2][2];
+};
+
+__device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+// tile (bi, j), bi >= j, of a walker's workspace (lower triangle incl. the diagonal)
+__device__ __forceinline__ long long tix(int bi, int j) { return (long long)bi * (bi + 1) / 2 + j; }
+// double offset of fragment pair (s, kk2) of `lane` in a fragment-layout tile
+__device__ __forceinline__ int fpair(int s, int kk2, int lane) { return ((s * 4 + kk2) * 64 + lane) * 2; }
+// double offset of element (row, col) in a fragment-layout tile
+__device__ __forceinline__ int felem(int row, int col) {
+    const int kk = col >> 2;
+    return fpair(row >> 4, kk >> 1, (col & 3) * 16 + (row & 15)) + (kk & 1);
+}
+
+__device__ __forceinline__ void park(double *tile, const Acc &a, int lane) {
+    double2 *T = reinterpret_cast<double2 *>(tile);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int ih = 0; ih < 2; ++ih)
+                T[((p * 2 + q) * 2 + ih) * 64 + lane] = make_double2(a.c[p][q][2 * ih], a.c[p][q][2 * ih + 1]);
+}
+__device__ __forceinline__ void unpark(const double *tile, Acc &a, int lane) {
+    const double2 *T = reinterpret_cast<const double2 *>(tile);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int ih = 0; ih < 2; ++ih) {
+                const double2 v = T[((p * 2 + q) * 2 + ih) * 64 + lane];
+                a.c[p][q][2 * ih] = v.x;
+                a.c[p][q][2 * ih + 1] = v.y;
+            }
+}
+// all 16 fragments of a fragment-layout tile: f[s][kk]
+__device__ __forceinline__ void load_frags(const double *tile, double (&f)[2][8], int lane) {
+    const double2 *T = reinterpret_cast<const double2 *>(tile);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int kk2 = 0; kk2 < 4; ++kk2) {
+            const double2 v = T[(s * 4 + kk2) * 64 + lane];
+            f[s][2 * kk2] = v.x;
+            f[s][2 * kk2 + 1] = v.y;
+        }
+}
+
+// Quasi-periodic covariance of two epochs tau apart (gp.py:126-156; tinygp ExpSineSquared x
+// ExpSquared, scaled by amp^2), fp64.
+struct QP {
+    double amp2, gam, inv_per, inv_le;
+};
+__device__ __forceinline__ double qp_cov(const QP &h, double tau) {
+    const double sn = sinpi(fabs(tau) * h.inv_per);
+    const double x = tau * h.inv_le;
+    return h.amp2 * exp(-(h.gam * (sn * sn) + 0.5 * (x * x)));
+}
+
+template <int NW, int MAXR, bool COND>   // MAXR tile rows per wave: nt <= MAXR * NW
+__global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
+    constexpr int NT = 64 * NW;
+    extern __shared__ double smem64[];
+    const int n = a.n, ni = a.ni, np = a.np;
+    const int nt = (n + TB - 1) / TB, npad = nt * TB;
+    double *Lt = smem64;              // [npad] epochs (padding: t[n-1])
+    double *Lr = Lt + npad;           // [npad] rhs r, reduced in place; segment k becomes y_k (then alpha_k)
+    double *Ldia = Lr + npad;         // [npad] velerr^2 + jit^2 (padding: 1)
+    double *fb = Ldia + npad;         // [TB][FS] the factor's row buffer; back substitution partial sums
+    double *li = fb + TB * FS;        // [TB][FS] -X = -L_kk^-1 of the step, fragment layout (first TILE);
+                                      //          the inverse's columns while the factor runs
+    double *red = li + TB * FS;       // [2 NW]
+    SC *tab = reinterpret_cast<SC *>(red + 2 * NW);
+    PlanetK *pks = reinterpret_cast<PlanetK *>(tab + kTabN);
+    int *oks = reinterpret_cast<int *>(pks + RVK_MAX_PLANETS);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wr = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave owns tile rows wr, wr + NW, ...
+    const EpochData &d = a.d;
+    const bool multi = ni > 1, tp = d.par == RVK_PAR_PKEWTP;
+    for (int i = tid; i < kTabN; i += NT) tab[i] = d.tab[i];
+    double *wk = a.work + (long long)blockIdx.x * a.work_stride;
+
+    for (long long w = blockIdx.x; w < a.W; w += gridDim.x) {
+        if (a.gate && !__builtin_isnan(a.gate[w])) continue;          // fallback: only the fp32 NaN walkers
+        if (!COND && a.post.lp && a.post.lp[w] == -INFINITY) {           // rejected before the likelihood
+            if (tid == 0) a.out[w] = -INFINITY;
+            continue;
+        }
+        const double *row = a.theta + w * a.stride;
+        const double *hp = a.hyper + w * a.hstride;
+        // ---- 1. planets, mean model, residuals -----------------------------------------------
+        if (tid < np) {
+            PlanetK pk;
+            const bool ok = tp ? planet_consts_t<0, true>(row + 5 * tid, pk, 0, tab) : planet_consts(d.par, row + 5 * tid, pk);
+            pks[tid] = pk;
+            oks[tid] = ok;
+        }
+        __syncthreads();   // (the table fill of the first trip lands here too)
+        bool alive = true;
+        for (int p = 0; p < np; ++p) alive &= oks[p] != 0;
+        if (!alive) {                                      // fit.py:8083-8085 / Planet() raises
+            if (COND) {
+                for (long long q = tid; q < a.T; q += NT) a.pred[w * a.T + q] = NAN;
+            } else if (tid == 0) {
+                a.out[w] = -INFINITY;
+            }
+            __syncthreads();
+            continue;
+        }
+        const double *g = row + 5 * np, *jit = g + ni;
+        const double gd = jit[ni], gdd = jit[ni + 1];
+        const QP h{hp[0] * hp[0], 1.0 / (2.0 * hp[2] * hp[2]), 1.0 / hp[3], 1.0 / hp[1]};
+        for (int i = tid; i < npad; i += NT) {
+            const double t = d.t[i < n ? i : n - 1];
+            Lt[i] = t;
+            double ri = 0.0, di = 1.0;
+            if (i < n) {
+                const int ii = multi ? d.inst[i] : 0;
+                double rv = 0.0;
+                for (int p = 0; p < np; ++p) rv = planet_rv<0>(pks[p], t, tab, rv);
+                const double dt = t - d.t0;
+                rv += __builtin_fma(gd, dt, gdd * (dt * dt));      // Trend (fit.py:8031-8035)
+                rv += g[ii];                                       // gamma (fit.py:8041-8045)
+                ri = d.vel[i] - rv;
+                di = d.s2[i] + jit[ii] * jit[ii];                  // fit.py:8096-8098
+            }
+            Lr[i] = ri;
+            Ldia[i] = di;
+        }
+        __syncthreads();
+        // ---- 2. pipelined blocked Cholesky -----------------------------------------------------
+        // -C(bi, bj)^T in C/D layout; padding rows/columns are identity
+        auto cov_tile = [&](int bi, int bj, Acc &A) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int gi = bi * TB + 16 * q + (lane & 15);
+                const double ti = Lt[gi], di = Ldia[gi];
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int gj = bj * TB + 16 * p + (lane >> 4) + 4 * i;
+                        const double kv = qp_cov(h, ti - Lt[gj]);
+                        const bool in = gi < n && gj < n, dg = gi == gj;
+                        const double v = in ? (dg ? kv + di : kv) : (dg ? 1.0 : 0.0);
+                        A.c[p][q][i] = -v;
+                    }
+            }
+        };
+        double quad = 0.0;          // sum of y^2 over this wave's lanes
+        double dpr = 1.0;           // product of this wave's pivots L_ii^2, renormalised (x 2^pexp)
+        int pexp = 0;
+        Acc nacc[MAXR], dacc;
+#pragma unroll
+        for (int q = 0; q < MAXR; ++q) {
+            const int bi = wr + NW * q;
+            if (bi < nt) {
+                Acc t;
+                cov_tile(bi, 0, t);
+                if (bi == 0) dacc = t;
+                else park(wk + tix(bi, 0) * TILE, t, lane);
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < nt; ++k) {
+            // ---- P(k): factor the diagonal tile (the owner of row k) ---------------------------
+            if (wr == k % NW) {
+                __builtin_amdgcn_s_setprio(1);    // the step's critical path goes first on its SIMD
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            fb[(16 * q + (lane & 15)) * FS + 16 * p + (lane >> 4) + 4 * i] = -dacc.c[p][q][i];
+                wave_lds_sync();
+                // lane i < 32 works on row i of acc(k, k) (fb, in place: it becomes row i of L_kk);
+                // lane 32 + j on column j of the identity (xb), which becomes column j of
+                // X = L_kk^-1 under the same updates (forward substitution).  Dynamic loops over
+                // LDS-resident vectors: the factor needs few registers, so nothing else has to
+                // leave them while it runs.
+                double *xb = li;   // li is free until the end of the factor (S1(k-1) read it before B2)
+                if (lane >= 32)
+                    for (int m = 0; m < TB; ++m) xb[m * FS + (lane - 32)] = m == lane - 32 ? 1.0 : 0.0;
+                wave_lds_sync();
+                double *vec = lane < 32 ? fb + lane * FS : xb + (lane - 32);
+                const int vs = lane < 32 ? 1 : FS;
+#pragma unroll 1
+                for (int r = 0; r < TB; ++r) {
+                    const int rr = __builtin_amdgcn_readfirstlane(r);
+                    const double *lrow = fb + rr * FS;           // row r of L (L[r][m], m < r: final)
+                    double v0 = vec[rr * vs], v1 = 0.0;
+                    int m = 0;
+#pragma unroll 1
+                    for (; m + 1 < rr; m += 2) {
+                        const double2 l2 = *reinterpret_cast<const double2 *>(lrow + m);
+                        v0 = __builtin_fma(-vec[m * vs], l2.x, v0);
+                        v1 = __builtin_fma(-vec[(m + 1) * vs], l2.y, v1);
+                    }
+                    if (m < rr) v0 = __builtin_fma(-vec[m * vs], lrow[m], v0);
+                    const double v = v0 + v1;
+                    const double piv = readlane_d(v, rr);        // L[r][r]^2 (<= 0 / NaN propagate)
+                    const double dd = __builtin_sqrt(piv);
+                    const double inv = 1.0 / dd;
+                    wave_lds_sync();                             // every lane has read row r
+                    vec[rr * vs] = lane == rr ? dd : v * inv;
+                    wave_lds_sync();
+                    dpr *= piv;
+                    if ((r & 7) == 7) {
+                        int e;
+                        dpr = __builtin_frexp(dpr, &e);
+                        pexp += e;
+                    }
+                }
+                double av[TB];
+                if (lane >= 32)
+#pragma unroll
+                    for (int r = 0; r < TB; ++r) av[r] = xb[r * FS + (lane - 32)];
+                wave_lds_sync();
+                if (lane >= 32) {                               // -X, fragment layout
+                    const int j = lane - 32, kk = j >> 2;
+#pragma unroll
+                    for (int r = 0; r < TB; ++r) {
+                        const int o = fpair(r >> 4, kk >> 1, (j & 3) * 16 + (r & 15)) + (kk & 1);
+                        li[o] = -av[r];
+                        if (COND) wk[tix(k, k) * TILE + o] = -av[r];   // kept for the back substitution
+                    }
+                }
+                wave_lds_sync();
+                if (lane < 32) {                                // y_k = X r_k, in place of r_k
+                    double y = 0.0;
+#pragma unroll
+                    for (int j = 0; j < TB; ++j) y = __builtin_fma(-li[felem(lane, j)], Lr[k * TB + j], y);
+                    quad += y * y;
+                    Lr[k * TB + lane] = y;
+                }
+                __builtin_amdgcn_s_setprio(0);
+            }
+#pragma unroll
+            for (int p = 0; p < 2; ++p)     // (dacc is dead until S2 sets it again)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) dacc.c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
+            // every accumulator is (re)defined here, after the factor: none is live across it
+#pragma unroll
+            for (int q = 0; q < MAXR; ++q)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq) nacc[q].c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
+            // ---- P(k): the next column's tiles, all but the j = k term --------------------------
+            if (k + 1 < nt) {
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q) {
+                    const int bi = wr + NW * q;
+                    if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
+                }
+                // operands: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows at a time,
+                // half a tile (4 of the 8 k-steps) per register set; sets X / Y alternate so the next
+                // half's loads are in flight during this half's MFMAs.  The trip past the end re-reads
+                // the last half (unconditional loads, exact waits).
+                auto pass = [&](auto q0c) {
+                    constexpr int Q0 = decltype(q0c)::value;
+                    constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
+                    bool any = false;
+#pragma unroll
+                    for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NW * q >= k + 1) && (wr + NW * q < nt);
+                    if (!any || k == 0) return;
+                    struct Ops {
+                        double2 a[2][2], b[R][2][2];
+                    };
+                    auto issue = [&](Ops &o, int hx) {
+                        const int hh = hx < 2 * k ? hx : 2 * k - 1;
+                        const int j = hh >> 1, half = hh & 1;
+                        const double2 *ta = reinterpret_cast<const double2 *>(wk + tix(k + 1, j) * TILE);
+#pragma unroll
+                        for (int s = 0; s < 2; ++s)
+#pragma unroll
+                            for (int u = 0; u < 2; ++u) o.a[s][u] = ta[(s * 4 + 2 * half + u) * 64 + lane];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int bi = wr + NW * (Q0 + r);
+                            const bool live = bi >= k + 1 && bi < nt;
+                            const double2 *tb = reinterpret_cast<const double2 *>(wk + tix(live ? bi : k + 1, j) * TILE);
+#pragma unroll
+                            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) o.b[r][s][u] = tb[(s * 4 + 2 * half + u) * 64 + lane];
+                        }
+                    };
+                    auto consume = [&](const Ops &o) {
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int bi = wr + NW * (Q0 + r);
+                            if (bi >= k + 1 && bi < nt) {
+                                Acc &acc = nacc[Q0 + r];
+#pragma unroll
+                                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                                    for (int cmp = 0; cmp < 2; ++cmp)
+#pragma unroll
+                                        for (int p = 0; p < 2; ++p)
+#pragma unroll
+                                            for (int q = 0; q < 2; ++q)
+                                                acc.c[p][q] = mfma64(cmp ? o.a[p][u].y : o.a[p][u].x,
+                                                                     cmp ? o.b[r][q][u].y : o.b[r][q][u].x, acc.c[p][q]);
+                            }
+                        }
+                    };
+                    Ops X, Y;
+                    issue(X, 0);
+                    for (int hx = 0; hx < 2 * k; hx += 2) {
+                        issue(Y, hx + 1);
+                        consume(X);
+                        issue(X, hx + 2);
+                        consume(Y);
+                    }
+                };
+                pass(std::integral_constant<int, 0>{});
+                if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
+                if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
+                if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
+            }
+            __syncthreads();                                // B1: -X and y_k published
+            if (k + 1 == nt) break;
+            // ---- S1(k): L(bi, k) = acc(bi, k) X^T, stored; rhs update --------------------------
+            {
+                double xa[2][8];
+                {
+                    const double2 *X2 = reinterpret_cast<const double2 *>(li);
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+#pragma unroll
+                        for (int kk2 = 0; kk2 < 4; ++kk2) {
+                            const double2 v = X2[(s * 4 + kk2) * 64 + lane];
+                            xa[s][2 * kk2] = v.x;
+                            xa[s][2 * kk2 + 1] = v.y;
+                        }
+                }
+                double yv[2][4];
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) yv[p][i] = Lr[k * TB + 16 * p + (lane >> 4) + 4 * i];
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q) {
+                    const int bi = wr + NW * q;
+                    if (bi > k && bi < nt) {
+                        double *T = wk + tix(bi, k) * TILE;
+                        Acc cur;
+                        unpark(T, cur, lane);
+                        Acc o;
+#pragma unroll
+                        for (int p = 0; p < 2; ++p)
+#pragma unroll
+                            for (int qq = 0; qq < 2; ++qq) o.c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
+                        // L(bi, k)^T = (-X) (-acc)^T: A = -X fragments, B = the parked C/D registers
+#pragma unroll
+                        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                                for (int qq = 0; qq < 2; ++qq)
+                                    o.c[p][qq] = mfma64(xa[p][kk], cur.c[kk >> 2][qq][kk & 3], o.c[p][qq]);
+                        // o.c[p][qq][i] at lane l = L(bi, k)[16 qq + (l & 15)][16 p + (l >> 4) + 4 i]
+                        //                         = frag(qq, 4 p + i)[l]
+                        double2 *T2 = reinterpret_cast<double2 *>(T);
+#pragma unroll
+                        for (int qq = 0; qq < 2; ++qq) {
+                            double s = 0.0;
+#pragma unroll
+                            for (int p = 0; p < 2; ++p) {
+#pragma unroll
+                                for (int ih = 0; ih < 2; ++ih)
+                                    T2[(qq * 4 + 2 * p + ih) * 64 + lane] = make_double2(o.c[p][qq][2 * ih], o.c[p][qq][2 * ih + 1]);
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) s = __builtin_fma(o.c[p][qq][i], yv[p][i], s);
+                            }
+                            s += __shfl_xor(s, 16);
+                            s += __shfl_xor(s, 32);
+                            if (lane < 16) Lr[bi * TB + 16 * qq + lane] -= s;
+                        }
+                    }
+                }
+            }
+            __syncthreads();                                // B2: L(k+1, k) published
+            // ---- S2(k): the j = k term; park for S1(k+1) ---------------------------------------
+            // (L(bi, k) is re-read from the workspace -- an L1/L2 hit -- rather than kept in
+            // registers from S1, which would not fit next to the accumulators)
+            {
+                double af[2][8];
+                load_frags(wk + tix(k + 1, k) * TILE, af, lane);
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q) {
+                    const int bi = wr + NW * q;
+                    if (bi > k && bi < nt) {
+                        double bf[2][8];
+                        load_frags(wk + tix(bi, k) * TILE, bf, lane);
+#pragma unroll
+                        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                                for (int qq = 0; qq < 2; ++qq)
+                                    nacc[q].c[p][qq] = mfma64(af[p][kk], bf[qq][kk], nacc[q].c[p][qq]);
+                        if (bi == k + 1) dacc = nacc[q];
+                        else park(wk + tix(bi, k + 1) * TILE, nacc[q], lane);
+                    }
+                }
+            }
+        }
+        if (!COND) {
+            // ---- 3. ll = -1/2 y.y - 1/2 sum log L_ii^2 - n/2 log 2 pi ---------------------------
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) quad += __shfl_xor(quad, o);
+            if (lane == 0) {
+                red[2 * wr] = quad;
+                red[2 * wr + 1] = log(dpr) + (double)pexp * kLn2;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double qs = 0.0, ls = 0.0;
+                for (int u = 0; u < NW; ++u) {
+                    qs += red[2 * u];
+                    ls += red[2 * u + 1];
+                }
+                double ll = -0.5 * qs - 0.5 * ls - 0.5 * (double)n * kLog2Pi;
+                if (!__builtin_isfinite(ll)) ll = NAN;             // not positive definite
+                if (a.post.lp) ll = (((ll + a.post.lp[w]) + a.post.lhp[w]) + a.post.jac) + a.post.renorm;
+                a.out[w] = ll;
+            }
+            __syncthreads();
+        } else {
+            // ---- 3'. alpha = L^-T y: alpha_k = X_kk^T (y_k - sum_{bi > k} L(bi, k)^T alpha_bi) -----
+            constexpr int G = NT / TB;
+            const int c = tid & (TB - 1), gq = tid / TB;
+            for (int k = nt - 1; k >= 0; --k) {
+                double part = 0.0;
+                for (int bi = k + 1 + gq; bi < nt; bi += G) {
+                    const double *T = wk + tix(bi, k) * TILE;
+#pragma unroll 8
+                    for (int r = 0; r < TB; ++r) part = __builtin_fma(T[felem(r, c)], Lr[bi * TB + r], part);
+                }
+                fb[gq * TB + c] = part;
+                __syncthreads();
+                if (tid < TB) {
+                    double z = Lr[k * TB + c];
+                    for (int u = 0; u < G; ++u) z -= fb[u * TB + c];
+                    fb[G * TB + c] = z;
+                }
+                __syncthreads();
+                if (tid < TB) {
+                    const double *X = wk + tix(k, k) * TILE;    // -X, fragment layout
+                    double al = 0.0;
+#pragma unroll 8
+                    for (int i = 0; i < TB; ++i) al = __builtin_fma(-X[felem(i, c)], fb[G * TB + i], al);
+                    Lr[k * TB + c] = al;
+                }
+                __syncthreads();
+            }
+            // mean(t_q) = sum_i k(t_q - t_i) alpha_i   (K(X_test, X) alpha; no diagonal term)
+            for (long long q = tid; q < a.T; q += NT) {
+                const double tq = a.tq[q];
+                double acc = 0.0;
+                for (int i = 0; i < n; ++i) acc = __builtin_fma(qp_cov(h, tq - Lt[i]), Lr[i], acc);
+                a.pred[w * a.T + q] = acc;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int NW, int MAXR, bool COND>
+void launch_gp64(hipStream_t st, unsigned grid, size_t lds, const Gp64Args &a) {
+    static size_t allowed = 0;   // dynamic LDS beyond the default needs the attribute
+    if (lds > allowed) {
+        (void)hipFuncSetAttribute((const void *)gp64_kernel<NW, MAXR, COND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        allowed = lds;
+    }
+    hipLaunchKernelGGL((gp64_kernel<NW, MAXR, COND>), dim3(grid), dim3(64 * NW), lds, st, a);
+}
+
+}  // namespace
+
+namespace rvk {
+
+Gp64Shape gp64_shape(int n) {
+    const int nt = (n + TB - 1) / TB;
+    return nt <= 16 ? Gp64Shape{8, 2} : Gp64Shape{8, 4};
+}
+
+size_t gp64_lds_bytes(int n, int nw) {
+    const int nt = (n + TB - 1) / TB;
+    size_t b = sizeof(double) * (3 * (size_t)nt * TB + 2 * TB * FS + 2 * (size_t)nw);
+    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
+    return b;
+}
+
+long long gp64_work_doubles(int n) {
+    const long long nt = (n + TB - 1) / TB;
+    return nt * (nt + 1) / 2 * TILE;
+}
+
+gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape sh) {
+    (void)multi;
+    (void)tp;
+    if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
+    if (sh.maxr == 2) return condition ? launch_gp64<8, 2, true> : launch_gp64<8, 2, false>;
+    return condition ? launch_gp64<8, 4, true> : launch_gp64<8, 4, false>;
+}
+
+}  // namespace rvk

@@ -41,8 +41,37 @@ def import_reference():
           jit=lambda f=None, **k: (f if f is not None else (lambda g: g)), numpy=jnp)
 
     class _Kernel:
-        pass
-    kern = _stub("tinygp.kernels", Kernel=_Kernel)
+        """tinygp 0.3 kernel algebra, restated for the GP goldens (the covariance the
+        reference's GPKernel.build_kernel describes, gp.py:126-156; tinygp is absent, so
+        this part is a restatement -- "parity unpinned" at the tinygp boundary)."""
+        def __mul__(self, other):
+            return _Product(self, other)
+
+        def __rmul__(self, other):
+            return _Product(other, self)
+
+    class _Product(_Kernel):
+        def __init__(self, a, b):
+            self.a, self.b = a, b
+
+        def evaluate(self, tau):
+            ev = lambda k: k.evaluate(tau) if isinstance(k, _Kernel) else k   # noqa: E731
+            return ev(self.a) * ev(self.b)
+
+    class ExpSquared(_Kernel):
+        def __init__(self, scale):
+            self.scale = scale
+
+        def evaluate(self, tau):
+            return np.exp(-0.5 * (tau / self.scale) ** 2)
+
+    class ExpSineSquared(_Kernel):
+        def __init__(self, scale, gamma):
+            self.scale, self.gamma = scale, gamma
+
+        def evaluate(self, tau):
+            return np.exp(-self.gamma * np.sin(np.pi * np.abs(tau) / self.scale) ** 2)
+    kern = _stub("tinygp.kernels", Kernel=_Kernel, ExpSquared=ExpSquared, ExpSineSquared=ExpSineSquared)
     _stub("tinygp", GaussianProcess=None, kernels=kern)
     _stub("emcee")
     _stub("corner")
@@ -316,9 +345,126 @@ def gen_51peg(ref):
     posterior_case(ref, "51peg", ds, th, free, spec)
 
 
+# --------------------------------------------------------------------------
+def _dense_gp_loglike(kernel, time_array, vel_array, verr_squared_array, mean_model):
+    """Stand-in for GPLogLikelihood._compute_gp_log_likelihood (fit.py:8045-8060): tinygp 0.3's
+    GaussianProcess(kernel, X, diag).log_probability(y) restated with a dense fp64 Cholesky
+    (DirectSolver).  Everything around it -- the mean model, the jitter diagonal, the posterior's
+    checks, priors, hyperpriors and corrections -- is the reference's own code."""
+    from scipy.linalg import cholesky, solve_triangular
+    t = np.asarray(time_array, np.float64)
+    K = kernel.evaluate(np.subtract.outer(t, t))
+    K[np.diag_indices(len(t))] += np.asarray(verr_squared_array)
+    r = np.asarray(vel_array) - np.asarray(mean_model)
+    try:
+        L = cholesky(K, lower=True, check_finite=False)
+    except np.linalg.LinAlgError:
+        return np.nan
+    alpha = solve_triangular(L, r, lower=True, check_finite=False)
+    return -0.5 * alpha @ alpha - np.sum(np.log(np.diag(L))) - 0.5 * len(t) * np.log(2 * np.pi)
+
+
+def gp_posterior_case(ref, name, ds, theta_full, hyper, free_names, free_hyper, priors_spec, hyper_spec,
+                      fixed_hyper):
+    """Evaluate the reference GPLogPosterior (fit.py:7596-7939) on every walker."""
+    import ravest.gp
+    names = ds.names
+    fixed = {n: float(ds.truth[n]) for n in names if n not in free_names}
+    priors = {k: prior_obj(ref, v) for k, v in priors_spec.items()}
+    hyperpriors = {k: prior_obj(ref, v) for k, v in hyper_spec.items()}
+    Pz = ref.param.Parameterisation(ds.parameterisation.parameterisation)
+    kern = ravest.gp.GPKernel("Quasiperiodic")
+    ref.fit.GPLogLikelihood._compute_gp_log_likelihood = staticmethod(_dense_gp_loglike)
+    gpost = ref.fit.GPLogPosterior(ds.planet_letters, Pz, kern, priors, hyperpriors, fixed, fixed_hyper,
+                                   list(free_names), list(free_hyper), ds.time, ds.vel, ds.velerr, ds.t0,
+                                   ds.instrument, list(ds.unique_instruments))
+    hnames = ["gp_amp", "gp_lambda_e", "gp_lambda_p", "gp_period"]
+    free_idx = [names.index(n) for n in free_names]
+    hidx = [hnames.index(n) for n in free_hyper]
+    x = np.concatenate([theta_full[:, free_idx], hyper[:, hidx]], axis=1)
+    lp = np.empty(len(x)); ll = np.empty(len(x))
+    for i in range(len(x)):
+        d = dict(zip(list(free_names) + list(free_hyper), x[i]))
+        lp[i] = gpost.log_probability(d)
+        allp = fixed | {n: d[n] for n in free_names}
+        allh = dict(fixed_hyper) | {n: d[n] for n in free_hyper}
+        try:
+            ll[i] = gpost.gp_log_likelihood(allp, allh)
+        except Exception:
+            ll[i] = np.nan
+    meta = {"name": name, "names": names, "free_names": list(free_names), "free_hyper": list(free_hyper),
+            "fixed": fixed, "fixed_hyper": dict(fixed_hyper), "priors": priors_spec, "hyperpriors": hyper_spec,
+            "planet_letters": ds.planet_letters, "parameterisation": ds.parameterisation.parameterisation,
+            "unique_instruments": list(ds.unique_instruments), "t0": ds.t0,
+            "jacobian": float(gpost._logprob_jacobian_correction),
+            "renorm": float(gpost._logprob_prior_renorm_correction)}
+    np.savez(os.path.join(OUT, f"gppost_{name}.npz"), time=ds.time, vel=ds.vel, velerr=ds.velerr,
+             inst_idx=ds.inst_idx, instrument=ds.instrument.astype("U16"), theta_full=theta_full, hyper=hyper,
+             x=x, log_prob=lp, log_like=ll, meta=np.array(json.dumps(meta)))
+    print(f"gp {name}: W={len(x)} N={len(ds.time)} finite={np.isfinite(lp).sum()} ll_finite={np.isfinite(ll).sum()}")
+
+
+def gen_gp_logpost(ref):
+    def hyper_block(rng, W):
+        return np.column_stack([rng.uniform(2, 6, W), rng.uniform(30, 120, W), rng.uniform(0.3, 1.0, W),
+                                rng.uniform(10, 40, W)])
+    hnames = ["gp_amp", "gp_lambda_e", "gp_lambda_p", "gp_period"]
+    # A: 1 planet, P K e w Tp, every hyperparameter free; invalid jitter / hyper / eccentricity rows
+    ds = make_dataset(1, 120, 1, seed=61)
+    rng = np.random.default_rng(61)
+    th = make_walkers(ds, 80, seed=61, scale=0.002)
+    th[:, ds.names.index("jit_HARPS")] = np.abs(th[:, ds.names.index("jit_HARPS")])
+    hy = hyper_block(rng, 80)
+    th[1, ds.names.index("jit_HARPS")] = -0.5          # jitter < 0
+    hy[2, 0] = -1.0                                     # gp_amp <= 0 (hyperparameter validity)
+    hy[3, 2] = 0.0                                      # gp_lambda_p == 0
+    hy[4, 1] = 500.0                                    # outside its hyperprior
+    th[5, ds.names.index("e_b")] = 1.2                  # invalid planet
+    free = [n for n in ds.names if n not in ("gd", "gdd")]
+    hspec = {"gp_amp": ("Uniform", {"lower": 0.0, "upper": 10.0}),
+             "gp_lambda_e": ("Uniform", {"lower": 1.0, "upper": 200.0}),
+             "gp_lambda_p": ("TruncatedNormal", {"mean": 0.6, "std": 0.3, "lower": 0.05, "upper": 2.0}),
+             "gp_period": ("Normal", {"mean": 25.0, "std": 10.0})}
+    gp_posterior_case(ref, "a", ds, th, hy, free, hnames, uniform_around(ds, free), hspec, {})
+    # B: 2 planets, 2 instruments, secosw/sesinw/Tc with U(-1, 1) priors (CASE_2), gp_period fixed
+    ds = make_dataset(2, 160, 2, seed=62, parameterisation="P K secosw sesinw Tc")
+    rng = np.random.default_rng(62)
+    th = make_walkers(ds, 64, seed=62, scale=0.002)
+    for inst in ds.unique_instruments:
+        j = ds.names.index(f"jit_{inst}")
+        th[:, j] = np.abs(th[:, j])
+    hy = hyper_block(rng, 64)
+    hy[:, 3] = 23.0
+    free = [n for n in ds.names if n not in ("gd", "gdd")]
+    fh = ["gp_amp", "gp_lambda_e", "gp_lambda_p"]
+    hspec = {"gp_amp": ("HalfNormal", {"std": 5.0}), "gp_lambda_e": ("Rayleigh", {"scale": 80.0}),
+             "gp_lambda_p": ("Uniform", {"lower": 0.1, "upper": 1.5})}
+    gp_posterior_case(ref, "b", ds, th, hy, free, fh, uniform_around(ds, free), hspec, {"gp_period": 23.0})
+    # C: CASE_3 -- secosw/sesinw/Tp sampled, priors on (e, w); trend free
+    ds = make_dataset(1, 200, 1, seed=63, parameterisation="P K secosw sesinw Tp", trend=True)
+    rng = np.random.default_rng(63)
+    th = make_walkers(ds, 48, seed=63, scale=0.002)
+    th[:, ds.names.index("jit_HARPS")] = np.abs(th[:, ds.names.index("jit_HARPS")])
+    th[3, ds.names.index("secosw_b")] = 0.9            # conversion ValueError (e >= 1)
+    th[3, ds.names.index("sesinw_b")] = 0.6
+    hy = hyper_block(rng, 48)
+    free = list(ds.names)
+    spec = {"e_b": ("Beta", {"a": 0.867, "b": 3.03}), "w_b": ("Uniform", {"lower": -np.pi, "upper": np.pi})}
+    for n, v in uniform_around(ds, [n for n in free if n.split("_")[0] not in ("secosw", "sesinw")]).items():
+        spec[n] = v
+    spec["gd"] = ("Normal", {"mean": 0.0, "std": 0.1})
+    spec["gdd"] = ("Normal", {"mean": 0.0, "std": 1e-3})
+    hspec = {k: ("Uniform", {"lower": 0.0, "upper": 500.0}) for k in hnames}
+    gp_posterior_case(ref, "c", ds, th, hy, free, hnames, spec, hspec, {})
+
+
 if __name__ == "__main__":
     ref = import_reference()
     os.makedirs(OUT, exist_ok=True)
+    if sys.argv[1:] == ["gp"]:
+        gen_gp_logpost(ref)
+        sys.exit(0)
+    gen_gp_logpost(ref)
     gen_kepler(ref)
     gen_planets(ref)
     gen_convert(ref)
