@@ -110,19 +110,35 @@ __device__ unsigned long long g_ll_trace[16][8];
 // SAMPLE (rvk_stretch_run): the rows are the proposals of the active half
 // (propose_kernel), lp their log-priors; after the reduction the wave accepts
 // or rejects its proposal and writes the walker's state and chain row.
+//
+// SAMPLE == 2 (fused proposals): each wave makes the stretch-move proposal of its walker
+// itself, lanes over coordinates, columns, prior slots and planets -- draws, q = c - (c - s) z,
+// the full row, the jitter check, the basic-kind priors (fit.py:3461-3482) and the planet
+// constants -- into its LDS slots, then runs the epoch loop: a half-step is one kernel instead
+// of propose_kernel + this one, and no block barrier separates a walker's prep from its loop.
+// Same arithmetic and order as propose_kernel / post_row_wave (rvk_post.hip,
+// rvk_post_dev.h), so the chain is the same bit for bit.
 template <int NP>
 struct PassCfg {
     static constexpr int WB = (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
 };
 
-template <int NP, bool MULTI, int SOLVER, bool TP, bool SAMPLE, int BLK = kBlock>
+template <int NP, bool MULTI, int SOLVER, bool TP, int SAMPLE, int BLK = kBlock>
 __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
                                                          long long stride, int wb, double *__restrict__ out,
                                                          PostArgs post, SampleArgs sa) {
     constexpr int WB = PassCfg<NP>::WB;
+    constexpr bool FUSE = SAMPLE == 2;
+    constexpr int WF = FUSE ? WB : 1;
     __shared__ PlanetK pks[WB][NP];
     __shared__ int okp[WB][NP];
+    __shared__ double fq[WF][kFuseMaxD], fx[WF][kFuseMaxD], ff[WF][kFuseMaxPFull];
+    constexpr int FP = FUSE ? kFuseMaxPFull : 1, FS = FUSE ? kFuseMaxPrior : 1;
+    __shared__ int fcol[FP];
+    __shared__ double ftm[FP];
+    __shared__ PriorSlot fsl[FS];
+    __shared__ double fterm[FUSE ? BLK / 64 : 1][FS];
     const int lane = threadIdx.x & 63;
     // Epoch data does not depend on the walker: this lane's first epoch is loaded once,
     // before anything else, so its latency hides under the table fill and the prep.
@@ -139,11 +155,46 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
 #endif
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // FUSE: a wave's proposal draws and reads of the walker rows (emcee's StretchMove), issued
+    // for the wave's first walker before the barrier so their latency hides under the table
+    // fill; the posterior's constants are staged in LDS (each is read in a loop with a runtime
+    // trip count: from global memory every iteration would wait on a load).
+    struct Fetch {
+        Draw dr;
+        double z, a, b, lpo;
+    };
+    auto fetch = [&](long long w) {
+        Fetch f;
+        const RunArgs &run = *sa.run;
+        const int D = sa.pd.n_free;
+        f.dr = draw(run, sa.step, sa.half, w, n_walkers);
+        const double zt = (run.a - 1.0) * f.dr.zu + 1.0;
+        f.z = zt * zt / run.a;
+        f.lpo = run.lp[f.dr.s];
+        f.a = f.b = 0.0;
+        if (lane < D) {
+            f.a = run.x[f.dr.s * D + lane];
+            f.b = run.x[f.dr.c * D + lane];
+        }
+        return f;
+    };
+    Fetch pre{};
+    if constexpr (FUSE) {
+        const long long w0 = (long long)blockIdx.x * wb + wv;
+        if (wv < wb && w0 < n_walkers) pre = fetch(w0);
+        for (int i = threadIdx.x; i < sa.pd.p_full; i += BLK) {
+            fcol[i] = sa.pd.colmap[i];
+            ftm[i] = sa.pd.tmpl[i];
+        }
+        for (int i = threadIdx.x; i < sa.pd.n_prior; i += BLK) fsl[i] = sa.pd.slots[i];
+        __syncthreads();   // (also publishes the table)
+    }
     LL_MARK(0);
     LL_MARK(1);
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
         // prep (the table fill above lands under the same barrier)
+        if constexpr (!FUSE) {
         for (int k = threadIdx.x; k < nb * NP; k += BLK) {
             const int j = k / NP, p = k - j * NP;
             const long long w = base + j;
@@ -156,16 +207,58 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         }
         LL_MARK(2);
         __syncthreads();
+        }
         LL_MARK(3);
         for (int j = wv; j < nb; j += BLK / 64) {
             const long long w = base + j;
-            const double *row = theta + w * stride;
-            const double lpw = post.lp ? post.lp[w] : 0.0;      // log-prior (posterior / sampler mode)
+            const double *row = FUSE ? ff[j] : theta + w * stride;
+            // log-prior (posterior / sampler mode)
+            double lpw = FUSE ? 0.0 : (post.lp ? post.lp[w] : 0.0);
             // SAMPLE: the accept test's operands are loaded before the epoch loop, so their latency
             // (sidx -> lp[sidx] is a dependent pair) hides under the loop instead of the wave's tail
             long long sw_s = 0;
             double lp_old_s = 0.0, fac_s = 0.0, au_s = 1.0;
-            if constexpr (SAMPLE) {
+            if constexpr (FUSE) {   // this wave's proposal (StretchMove.get_proposal + fit.py:3461-3482)
+                const PostDev &pd = sa.pd;
+                const int D = pd.n_free;
+                const Fetch f = (base == (long long)blockIdx.x * wb && j == wv) ? pre : fetch(w);
+                const Draw dr = f.dr;
+                const double z = f.z;
+                lp_old_s = f.lpo;                         // (needed only in the epilogue)
+                if (lane < D) {
+                    fq[j][lane] = f.b - (f.b - f.a) * z;
+                    fx[j][lane] = f.a;
+                }
+                wave_lds_sync();
+                if (lane < pd.p_full) {
+                    const int f = fcol[lane];
+                    ff[j][lane] = f >= 0 ? fq[j][f] : ftm[lane];
+                }
+                wave_lds_sync();
+                bool dead = false;
+                if (lane < pd.n_inst) dead = ff[j][5 * pd.n_planets + pd.n_inst + lane] < 0.0;   // fit.py:3465-3468
+                if (lane < pd.n_prior) {
+                    const PriorSlot &sl = fsl[lane];
+                    fterm[wv][lane] = prior_lp_basic(sl.kind, sl.p, ff[j][sl.src]);
+                }
+                if (lane < NP) {
+                    PlanetK pk;
+                    const double *p5 = ff[j] + 5 * lane;
+                    const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
+                    pks[j][lane] = pk;
+                    okp[j][lane] = ok;
+                }
+                wave_lds_sync();
+                dead = __builtin_amdgcn_ballot_w64(dead) != 0;
+                double lp = 0.0;
+                for (int k = 0; k < pd.n_prior; ++k) lp += fterm[wv][k];                      // the reference's key order
+                if (!isfinite(lp)) dead = true;                                                // fit.py:3481-3482
+                lpw = dead ? -INFINITY : lp;
+                fac_s = ((double)D - 1.0) * log(z);
+                au_s = dr.au;
+                sw_s = dr.s;
+                LL_MARK(2);
+            } else if constexpr (SAMPLE != 0) {
                 sw_s = sa.sidx[w];
                 // (a global-address-space load: a flat one would also hold lgkmcnt, which the
                 // epoch loop's LDS reads wait on)
@@ -276,21 +369,21 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             double tot = wave_sum(chi2 + lsum);
             LL_MARK(5);
             res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
-            if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
+            if (FUSE || post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
             }
-            if constexpr (SAMPLE) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
+            if constexpr (SAMPLE != 0) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
                 const RunArgs &run = *sa.run;
                 const int D = sa.D;
                 const long long sw = sw_s;
                 const double lp_old = lp_old_s;
                 const bool acc = fac_s + res - lp_old > log(au_s);
                 double *xs = run.x + sw * D;
-                const double *qw = sa.q + w * D;
+                const double *qw = FUSE ? fq[j] : sa.q + w * D;
                 const long long W2 = 2 * n_walkers;
                 double *chain = run.chain ? run.chain + (long long)sa.step * W2 * D : nullptr;
                 if (lane == 0 && isnan(res)) atomicOr(run.status, 1);
                 for (int c = lane; c < D; c += 64) {
-                    const double v = acc ? qw[c] : xs[c];
+                    const double v = acc ? qw[c] : (FUSE ? fx[j][c] : xs[c]);
                     if (acc) xs[c] = v;
                     if (chain) chain[sw * D + c] = v;
                 }
@@ -580,12 +673,12 @@ void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, lon
     int wb;
     if (NP == 1 && RVK_LL_BLOCK > kBlock && W >= 256LL * (RVK_LL_BLOCK / 64)) {   // >= one block per CU
         ll_grid<NP>(W, blocks, wb, RVK_LL_BLOCK / 64);
-        hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, false, RVK_LL_BLOCK>), dim3((unsigned)blocks),
+        hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, 0, RVK_LL_BLOCK>), dim3((unsigned)blocks),
                            dim3(RVK_LL_BLOCK), 0, st, d, n, ni, th, W, stride, wb, out, post, SampleArgs{});
         return;
     }
     ll_grid<NP>(W, blocks, wb);
-    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d,
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, SOLVER, TP, 0>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d,
                        n, ni, th, W, stride, wb, out, post, SampleArgs{});
 }
 
@@ -596,7 +689,18 @@ void launch_sample(hipStream_t st, EpochData d, int n, int ni, const double *row
     long long blocks;
     int wb;
     ll_grid<NP>(H, blocks, wb);
-    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, 1>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
+                       ni, rows, H, stride, wb, nullptr, post, sa);
+}
+
+// The same with the proposals made in the kernel's prep (SAMPLE == 2; rows unused).
+template <int NP, bool MULTI, bool TP>
+void launch_sample_fused(hipStream_t st, EpochData d, int n, int ni, const double *rows, long long H, long long stride,
+                         PostArgs post, const SampleArgs &sa) {
+    long long blocks;
+    int wb;
+    ll_grid<NP>(H, blocks, wb);
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, 2>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
                        ni, rows, H, stride, wb, nullptr, post, sa);
 }
 
@@ -625,24 +729,25 @@ loglike_launch_t pick_ll(int np, bool multi, int solver, bool tp) {
     return tp ? pick_ll_t<0, true>(np, multi) : pick_ll_t<0, false>(np, multi);
 }
 
-template <bool MULTI, bool TP>
+template <bool MULTI, bool TP, bool FUSED>
 sample_launch_t pick_sample_s(int np) {
     switch (np) {
-        case 1: return launch_sample<1, MULTI, TP>;
-        case 2: return launch_sample<2, MULTI, TP>;
-        case 3: return launch_sample<3, MULTI, TP>;
-        case 4: return launch_sample<4, MULTI, TP>;
-        case 5: return launch_sample<5, MULTI, TP>;
-        case 6: return launch_sample<6, MULTI, TP>;
-        case 7: return launch_sample<7, MULTI, TP>;
-        case 8: return launch_sample<8, MULTI, TP>;
+        case 1: return FUSED ? launch_sample_fused<1, MULTI, TP> : launch_sample<1, MULTI, TP>;
+        case 2: return FUSED ? launch_sample_fused<2, MULTI, TP> : launch_sample<2, MULTI, TP>;
+        case 3: return FUSED ? launch_sample_fused<3, MULTI, TP> : launch_sample<3, MULTI, TP>;
+        case 4: return FUSED ? launch_sample_fused<4, MULTI, TP> : launch_sample<4, MULTI, TP>;
+        case 5: return FUSED ? nullptr : launch_sample<5, MULTI, TP>;   // (fused: NP <= 4)
+        case 6: return FUSED ? nullptr : launch_sample<6, MULTI, TP>;   // (fused: NP <= 4)
+        case 7: return FUSED ? nullptr : launch_sample<7, MULTI, TP>;   // (fused: NP <= 4)
+        case 8: return FUSED ? nullptr : launch_sample<8, MULTI, TP>;   // (fused: NP <= 4)
         default: return nullptr;
     }
 }
 
+template <bool FUSED>
 sample_launch_t pick_sample(int np, bool multi, bool tp) {
-    if (multi) return tp ? pick_sample_s<true, true>(np) : pick_sample_s<true, false>(np);
-    return tp ? pick_sample_s<false, true>(np) : pick_sample_s<false, false>(np);
+    if (multi) return tp ? pick_sample_s<true, true, FUSED>(np) : pick_sample_s<true, false, FUSED>(np);
+    return tp ? pick_sample_s<false, true, FUSED>(np) : pick_sample_s<false, false, FUSED>(np);
 }
 
 int check_gfx950(int dev) {
@@ -776,7 +881,8 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->par = par;
     h->t0 = t0;
     h->launch = pick_ll(n_planets, n_inst > 1, 0, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample = pick_sample(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample = pick_sample<false>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_fused = pick_sample<true>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;

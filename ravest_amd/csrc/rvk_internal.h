@@ -88,6 +88,7 @@ struct rvk_handle {
     size_t cap_theta = 0, cap_out = 0, cap_tq = 0, cap_iq = 0;
     rvk::loglike_launch_t launch = nullptr;
     rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
+    rvk::sample_launch_t sample_fused = nullptr;   // ... with the proposals made in the same kernel
     int solver = 0;
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW

@@ -10,6 +10,7 @@
 // proposal in front of that (same thread) and an accept kernel behind it;
 // all state stays in HBM between steps.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -118,6 +119,7 @@ struct rvk_post {
     rvk_handle *h = nullptr;
     int n_free = 0, n_prior = 0;
     bool convert = false;
+    bool fusable = false;                  // proposals can be made inside the likelihood kernel
     double jac = 0.0, renorm = 0.0;
     int32_t *d_colmap = nullptr;
     double *d_tmpl = nullptr;
@@ -147,12 +149,18 @@ static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
     rvk_handle *h = p->h;
     const PostDev pd = p->dev();
     const PostArgs post{p->d_lp, p->jac, p->renorm};
+    const bool fused = p->fusable && h->solver == 0 && h->sample_fused;
     for (int s = 0; s < n; ++s)
         for (int half = 0; half < 2; ++half) {
+            if (fused) {   // one kernel per half-step: proposals in the likelihood kernel's prep
+                const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd};
+                h->sample_fused(st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
+                continue;
+            }
             hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, s, half, H,
                                p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
             if (h->solver == 0 && h->sample) {
-                const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s};
+                const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s, half, pd};
                 h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
             } else {
                 h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
@@ -262,6 +270,14 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
     p->n_free = n_free;
     p->n_prior = n_prior;
     p->convert = convert;
+    // The fused sampler path (loglike_kernel SAMPLE == 2) stages a walker's proposal and full
+    // row in LDS and evaluates the basic prior kinds inline; RVK_SAMPLER_FUSE=0 (experiment
+    // hook) keeps the two-kernel path.
+    bool basic = true;
+    for (int k = 0; k < n_prior; ++k) basic &= kind[k] <= kMaxBasicPriorKind;
+    const char *fe = getenv("RVK_SAMPLER_FUSE");
+    p->fusable = basic && !convert && n_free <= kFuseMaxD && pf <= kFuseMaxPFull && n_prior <= kFuseMaxPrior &&
+                 !(fe && atoi(fe) == 0);
     p->jac = jac;
     p->renorm = renorm;
     HIPCHK(hipSetDevice(h->device));

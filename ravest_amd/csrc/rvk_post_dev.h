@@ -40,10 +40,12 @@ __device__ __forceinline__ double rayleigh_lp(double x, double scale, double log
     return (log(y) - 0.5 * y * y) - log_scale;             // log(r) - 0.5 * r * r
 }
 
-// One prior term, the reference's formula and bounds (prior.py).
-inline __device__ double prior_lp(const PriorSlot &s, double x) {
-    const double *p = s.p;
-    switch (s.kind) {
+// The prior kinds whose log-density needs no transcendental function (Uniform,
+// EccentricityUniform, Normal, TruncatedNormal, HalfNormal: their logs are host constants);
+// the fused sampler (loglike_kernel SAMPLE == 2) evaluates these inline.
+constexpr int kMaxBasicPriorKind = RVK_PRIOR_HALFNORMAL;
+__device__ __forceinline__ double prior_lp_basic(int kind, const double *p, double x) {
+    switch (kind) {
         case RVK_PRIOR_UNIFORM:
             return (x < p[0] || x > p[1]) ? -INFINITY : p[2];
         case RVK_PRIOR_ECC_UNIFORM:
@@ -60,6 +62,16 @@ inline __device__ double prior_lp(const PriorSlot &s, double x) {
         case RVK_PRIOR_HALFNORMAL:
             if (x < 0.0) return -INFINITY;
             return halfnorm_lp(x, p[0], p[1], p[2]);
+        default:
+            return NAN;
+    }
+}
+
+// One prior term, the reference's formula and bounds (prior.py).
+inline __device__ double prior_lp(const PriorSlot &s, double x) {
+    const double *p = s.p;
+    if (s.kind <= kMaxBasicPriorKind) return prior_lp_basic(s.kind, p, x);
+    switch (s.kind) {
         case RVK_PRIOR_RAYLEIGH:
             if (x < 0.0) return -INFINITY;
             return rayleigh_lp(x, p[0], p[1]);
@@ -253,6 +265,15 @@ struct SampleArgs {
     const long long *sidx;      // [H] walker index of proposal w
     const RunArgs *run;         // state, chain and status pointers
     int step;                   // step within the chunk
+    int half;                   // active half (fused proposals, SAMPLE == 2)
+    PostDev pd;                 // the posterior (fused proposals, SAMPLE == 2)
 };
+
+// Limits of the fused proposal path (loglike_kernel SAMPLE == 2): the proposal, its full row
+// and the old state are staged in LDS per walker of a pass; priors basic kinds only, no
+// prior-side conversion.
+constexpr int kFuseMaxD = 16;
+constexpr int kFuseMaxPFull = 32;
+constexpr int kFuseMaxPrior = 32;
 
 }  // namespace rvk
