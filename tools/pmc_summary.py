@@ -11,11 +11,14 @@ out_dir, cfg = sys.argv[1], sys.argv[2]
 kfilter = sys.argv[3] if len(sys.argv) > 3 else None   # kernel-name substring (default: the plain loglike launch)
 
 def plain_loglike(name):
-    """loglike_kernel<NP, MULTI, SOLVER, TP, SAMPLE[, BLK]> with SAMPLE = false (not the sampler's)."""
+    """loglike_kernel<NP, MULTI, SOLVER, TP, SAMPLE[, BLK]> with SAMPLE = 0 (not the sampler's), or
+    the segmented loglike_seg_kernel the launcher picks for W >= 8192 (configs 3 and 4)."""
+    if "loglike_seg_kernel<" in name:
+        return True
     if "loglike_kernel<" not in name:
         return False
     args = name.split("loglike_kernel<", 1)[1].split(">(", 1)[0].split(", ")
-    return len(args) >= 5 and args[4] == "false"
+    return len(args) >= 5 and args[4] in ("false", "0")
 
 
 vals = defaultdict(lambda: defaultdict(float))
