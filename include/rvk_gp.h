@@ -106,6 +106,15 @@ int rvk_gp_logpost_device(rvk_gp_post *p, const double *d_free, int64_t n_walker
                           double *d_out, void *stream);
 int rvk_gp_logpost(rvk_gp_post *p, const double *free, int64_t n_walkers, int64_t row_stride, double *out);
 
+/* Device-resident stretch move over the GP log-posterior (GPFitter.run_mcmc's emcee
+ * EnsembleSampler with the default StretchMove(a=2), fit.py:4982-4990): the same contract,
+ * draws and chain layout as rvk_stretch_run (include/rvk_post.h) -- per half-step the
+ * proposals, rvk_gp_logpost_device on them, and the accept / reject, all stream-ordered. */
+int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t n_steps, double a,
+                       uint64_t seed, uint64_t step0, const int32_t *d_set, const double *d_zu,
+                       const int32_t *d_rint, const double *d_au, double *d_chain, double *d_lnp,
+                       int64_t *d_naccepted, int32_t *d_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,33 +76,6 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs 
     }
 }
 
-// Accept / reject (RedBlueMove.propose + update) and the chain write of the half, for the
-// unfused path (reference solver): one thread per proposal.
-__global__ __launch_bounds__(256) void accept_kernel(const RunArgs *__restrict__ runp, int step, long long H, int D,
-                                                     const double *__restrict__ q, const double *__restrict__ fac,
-                                                     const double *__restrict__ au,
-                                                     const long long *__restrict__ sidx,
-                                                     const double *__restrict__ nlp_all) {
-    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= H) return;
-    const RunArgs &run = *runp;
-    const long long s = sidx[j];
-    const double nlp = nlp_all[j];
-    if (isnan(nlp)) atomicOr(run.status, 1);
-    const double lnpdiff = fac[j] + nlp - run.lp[s];
-    double *xs = run.x + s * D;
-    if (lnpdiff > log(au[j])) {
-        for (int k = 0; k < D; ++k) xs[k] = q[j * D + k];
-        run.lp[s] = nlp;
-        if (run.nacc) run.nacc[s] += 1;
-    }
-    if (run.chain)
-        for (int k = 0; k < D; ++k) run.chain[((long long)step * 2 * H + s) * D + k] = xs[k];
-    if (run.lnpc) run.lnpc[(long long)step * 2 * H + s] = run.lp[s];
-}
-
-__global__ void set_run_kernel(RunArgs *dst, RunArgs v) { *dst = v; }
-
 unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
 
 constexpr int kStepsPerGraph = 8;   // steps per cached graph replay (4 or 6 kernels each)
@@ -164,7 +137,7 @@ static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
                 h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
             } else {
                 h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
-                hipLaunchKernelGGL(accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, p->d_run, s, H, p->n_free,
+                hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, p->d_run, s, H, p->n_free,
                                    p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_nlp);
             }
         }

@@ -276,4 +276,32 @@ constexpr int kFuseMaxD = 16;
 constexpr int kFuseMaxPFull = 32;
 constexpr int kFuseMaxPrior = 32;
 
+// Accept / reject (RedBlueMove.propose + update) and the chain write of the half, for the
+// unfused path (reference solver) and the GP sampler: one thread per proposal.
+static __global__ __launch_bounds__(256) void stretch_accept_kernel(const RunArgs *__restrict__ runp, int step, long long H, int D,
+                                                     const double *__restrict__ q, const double *__restrict__ fac,
+                                                     const double *__restrict__ au,
+                                                     const long long *__restrict__ sidx,
+                                                     const double *__restrict__ nlp_all) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= H) return;
+    const RunArgs &run = *runp;
+    const long long s = sidx[j];
+    const double nlp = nlp_all[j];
+    if (isnan(nlp)) atomicOr(run.status, 1);
+    const double lnpdiff = fac[j] + nlp - run.lp[s];
+    double *xs = run.x + s * D;
+    if (lnpdiff > log(au[j])) {
+        for (int k = 0; k < D; ++k) xs[k] = q[j * D + k];
+        run.lp[s] = nlp;
+        if (run.nacc) run.nacc[s] += 1;
+    }
+    if (run.chain)
+        for (int k = 0; k < D; ++k) run.chain[((long long)step * 2 * H + s) * D + k] = xs[k];
+    if (run.lnpc) run.lnpc[(long long)step * 2 * H + s] = run.lp[s];
+}
+
+static __global__ void set_run_kernel(RunArgs *dst, RunArgs v) { *dst = v; }
+
+
 }  // namespace rvk

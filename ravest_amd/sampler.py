@@ -136,15 +136,23 @@ class EnsembleSampler(_ChainMixin):
 class DeviceEnsembleSampler(_ChainMixin):
     """The stretch move with every sub-step on the GPU (include/rvk_post.h rvk_stretch_run).
 
-    ``log_posterior`` is a ``posterior.LogPosterior`` (or its ``DevicePosterior``);
-    its priors must be built-in prior classes.  The walker state, the chain and
-    the log-probabilities live in HBM; ``get_chain`` copies them to the host."""
+    ``log_posterior`` is a ``posterior.LogPosterior`` (or its ``DevicePosterior``), or a
+    ``gp.GPLogPosterior`` (or its ``DeviceGPPosterior``: GPFitter.run_mcmc's sampler,
+    rvk_gp_stretch_run); its priors must be built-in prior classes.  The walker state,
+    the chain and the log-probabilities live in HBM; ``get_chain`` copies them to the host."""
 
     def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed=None, rng: str = "philox",
                  steps_per_call: int = 256) -> None:
         import torch
+        from .gp import DeviceGPPosterior, GPLogPosterior
         from .posterior import DevicePosterior
-        self.post = log_posterior if isinstance(log_posterior, DevicePosterior) else DevicePosterior(log_posterior)
+        if isinstance(log_posterior, (DevicePosterior, DeviceGPPosterior)):
+            self.post = log_posterior
+        elif isinstance(log_posterior, GPLogPosterior):
+            self.post = DeviceGPPosterior(log_posterior)
+        else:
+            self.post = DevicePosterior(log_posterior)
+        self._run_fn = "rvk_gp_stretch_run" if isinstance(self.post, DeviceGPPosterior) else "rvk_stretch_run"
         ndim = self.post.n_free
         if nwalkers < 2 * ndim:
             raise ValueError(f"nwalkers ({nwalkers}) must be at least 2 * ndim ({2 * ndim})")
@@ -188,7 +196,7 @@ class DeviceEnsembleSampler(_ChainMixin):
                 draws = [torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in steps]))).to(dev)
                          for k in range(4)]
             ptr = (lambda t: t.data_ptr()) if draws else (lambda t: 0)
-            _lib.check(L.rvk_stretch_run(self.post._p, x.data_ptr(), lp.data_ptr(), W, n, self.a,
+            _lib.check(getattr(L, self._run_fn)(self.post._p, x.data_ptr(), lp.data_ptr(), W, n, self.a,
                                          getattr(self, "seed", 0), self.iteration + done,
                                          ptr(draws[0]) if draws else 0, ptr(draws[1]) if draws else 0,
                                          ptr(draws[2]) if draws else 0, ptr(draws[3]) if draws else 0,
