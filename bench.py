@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TF = 78.6     # MI355X FP64 vector peak (spec; half the FP32 vector rate)
 FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), dense
+FP64_MATRIX_PEAK_TF = 78.6     # MI355X FP64 matrix peak (spec; v_mfma_f64_16x16x4_f64), dense
 BYTES_PER_WALKER_EPOCH = 28    # t, v, sigma fp64 + int32 inst
 
 
@@ -89,7 +90,7 @@ def cpu_baseline(ds, theta, budget_s):
             r2 += 1
     el2 = time.perf_counter() - t2
     return {"value": solves / el, "unit": "Kepler solves/s", "cores": used, "kind": "port",
-            "host_cpus": host_cpu_info(),
+            "per_core_value": solves / el / max(1, used), "host_cpus": host_cpu_info(),
             "sample": f"{reps} x {len(sample)} walkers x {n_ep} epochs x {n_pl} planet(s) of the same "
                       f"config-{ds.cfg} ensemble, C oracle (oracle/rv_oracle.c, fp64, OpenMP), {el:.1f} s",
             "single_core_value": r1 * len(one) * n_ep * n_pl / el1,
@@ -101,7 +102,9 @@ def cpu_baseline(ds, theta, budget_s):
 def host_threads() -> int:
     """Threads for the CPU baseline: every CPU this process may run on (sched_getaffinity),
     but no more than the job's CPU share when the launcher states one (OMP_NUM_THREADS: the
-    GPU pool sets it to the 16 CPUs one GPU's job may use; its nproc shows the whole host)."""
+    GPU pool sets it to the 16 CPUs one GPU's job may use, and its rules forbid worker pools
+    beyond that share; nproc there shows the whole multi-GPU host, which other GPUs' jobs
+    share).  The line reports both counts (cpu_baseline.host_cpus) and the per-core rate."""
     n = len(os.sched_getaffinity(0))
     share = os.environ.get("OMP_NUM_THREADS")
     if share and share.isdigit() and int(share) > 0:
@@ -361,8 +364,24 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     with threadpool_limits(1):
         gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:2], hy[:2])
         t0 = time.perf_counter()
-        gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:k], hy[:k])
+        ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:k], hy[:k])
         cpu_s = (time.perf_counter() - t0) / k
+    # the reference's precision (fp64 throughout, RVK_GP_FP64): same batch, same timing method
+    gp64 = GPLogLikelihood(ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments,
+                           ds.planet_letters, ds.parameterisation, GPKernel("Quasiperiodic"),
+                           device=torch.cuda.current_device(), precision="fp64")
+    out64 = torch.empty(W, dtype=torch.float64, device=dev)
+    gp64.device(tt, ht, out64, st)
+    a.record(st)
+    for _ in range(2):
+        gp64.device(tt, ht, out64, st)
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    ms64 = a.elapsed_time(b) / 2
+    tf64 = flop / (ms64 * 1e-3) / 1e12
+    o64, o32 = out64.cpu().numpy()[:k], out.cpu().numpy()[:k]
+    fin = np.isfinite(ref)
+    rel = lambda x: float(np.max(np.abs(x[fin] - ref[fin]) / np.abs(ref[fin]))) if fin.any() else 0.0   # noqa: E731
     return {"config": f"config 5: 1 planet + quasi-periodic GP, {n} epochs, {W} walkers, fp32 factorisation",
             "ms_per_eval": ms, "walker_evals_per_s": W / (ms * 1e-3),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
@@ -371,6 +390,13 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
                                  "L2 memory-side bytes per launch (PMC, profiles/pmc_config5.json; includes "
                                  "Infinity-Cache hits: the workspace tiles re-read by the left-looking update)"},
             "n_masked_walkers": int((~np.isfinite(out.cpu().numpy())).sum()),
+            "precision": "fp32 factorisation, fp64 re-evaluation of walkers it rejects (default)",
+            "max_rel_err_vs_fp64_oracle": rel(o32),
+            "fp64": {"ms_per_eval": ms64, "walker_evals_per_s": W / (ms64 * 1e-3),
+                     "roofline": {"bound": "mfma", "achieved": tf64, "peak": FP64_MATRIX_PEAK_TF, "unit": "TFLOP/s",
+                                  "frac": tf64 / FP64_MATRIX_PEAK_TF},
+                     "max_rel_err_vs_fp64_oracle": rel(o64),
+                     "mask_identical": bool(np.array_equal(np.isfinite(o64), fin))},
             "cpu_baseline": {"value": 1.0 / cpu_s, "unit": "walker evals/s", "cores": 1, "kind": "port",
                              "sample": f"{k} walkers, fp64 restatement (oracle/gp_oracle.py, scipy LAPACK, 1 thread)"}}
 
