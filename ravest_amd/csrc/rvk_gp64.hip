@@ -41,6 +41,19 @@ using namespace rvk;
 
 namespace {
 
+#ifndef RVK_GP64_TRACE
+#define RVK_GP64_TRACE 0  // timing experiments only: s_memtime per phase, first walker of block 0
+#endif
+#if RVK_GP64_TRACE
+__device__ unsigned long long g_gp64_trace[8][32][8];
+#define G64_MARK(k, slot)                                                                             \
+    do {                                                                                              \
+        if (blockIdx.x == 0 && w == 0 && lane == 0 && (k) < 32) g_gp64_trace[wr][k][slot] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define G64_MARK(k, slot) do {} while (0)
+#endif
+
 constexpr int TB = 32;            // tile edge
 constexpr int TILE = TB * TB;     // doubles per tile
 constexpr int FS = 34;            // row stride (doubles) of the factor's row buffer: 16-byte aligned rows
@@ -113,7 +126,85 @@ __device__ __forceinline__ double qp_cov(const QP &h, double tau) {
     return h.amp2 * exp(-(h.gam * (sn * sn) + 0.5 * (x * x)));
 }
 
-template <int NW, int MAXR, bool COND>   // MAXR tile rows per wave: nt <= MAXR * NW
+// The diagonal factor of one step, one wave (its own register allocation: a 32-double row or
+// inverse column per lane never shares the register file with the accumulators).  fb holds
+// acc(k, k) row-major on entry and the rows of L_kk on exit; li gets -X = -L_kk^-1 in
+// fragment layout (and xdiag, if set); r_k = Lr[0..31] is replaced by y_k = X r_k.
+struct FactorAcc {
+    double quad, dpr;
+    int pexp;
+};
+using lds_d = __attribute__((address_space(3))) double;
+__device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li, lds_d *Lr, double *xdiag,
+                                                           FactorAcc fa) {
+    const int lane = threadIdx.x & 63;
+    double quad = fa.quad, dpr = fa.dpr;
+    int pexp = fa.pexp;
+    // lane i < 32: row i of acc(k, k); lane 32 + j: column j of the identity, turned into
+    // column j of X = L_kk^-1 by the same updates (forward substitution).  Row r of L
+    // (L[r][m], m < r, written by lane r at steps m) is read back as LDS broadcasts.
+    double av[TB];
+    const int lr = lane < 32 ? lane : 0;
+#pragma unroll
+    for (int m = 0; m < TB; ++m) {
+        const double x = fb[lr * FS + m];
+        av[m] = lane < 32 ? x : (m == lane - 32 ? 1.0 : 0.0);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < TB; ++r) {
+        // row r of L: every read issued before the first use (one wait, not one per element).
+        // LDS operations of one wave complete in order, so this step's reads see the previous
+        // steps' column writes without a fence.
+        double lrow[TB];
+#pragma unroll
+        for (int m = 0; m < r; ++m) lrow[m] = fb[r * FS + m];
+        double v0 = av[r], v1 = 0.0, v2 = 0.0, v3 = 0.0;
+#pragma unroll
+        for (int m = 0; m < r; ++m) {
+            if ((m & 3) == 0) v0 = __builtin_fma(-av[m], lrow[m], v0);
+            else if ((m & 3) == 1) v1 = __builtin_fma(-av[m], lrow[m], v1);
+            else if ((m & 3) == 2) v2 = __builtin_fma(-av[m], lrow[m], v2);
+            else v3 = __builtin_fma(-av[m], lrow[m], v3);
+        }
+        const double v = (v0 + v1) + (v2 + v3);
+        const double piv = readlane_d(v, r);        // L[r][r]^2 (<= 0 / NaN propagate)
+        // 1 / sqrt(piv): v_rsq_f64 and two Newton steps (quadratic: ~1 ulp), no IEEE sqrt + divide
+        // sequence on the step's critical path
+        double y = __builtin_amdgcn_rsq(piv);
+        y = y * __builtin_fma(-0.5 * piv, y * y, 1.5);
+        y = y * __builtin_fma(-0.5 * piv, y * y, 1.5);
+        av[r] = lane == r ? piv * y : v * y;
+        if (lane < 32) fb[lane * FS + r] = av[r];   // column r of L
+        dpr *= piv;
+        if ((r & 7) == 7) {
+            int e;
+            dpr = __builtin_frexp(dpr, &e);
+            pexp += e;
+        }
+    }
+    wave_lds_sync();
+    if (lane >= 32) {                               // -X, fragment layout
+        const int j = lane - 32, kk = j >> 2;
+#pragma unroll
+        for (int r = 0; r < TB; ++r) {
+            const int o = fpair(r >> 4, kk >> 1, (j & 3) * 16 + (r & 15)) + (kk & 1);
+            li[o] = -av[r];
+            if (xdiag) xdiag[o] = -av[r];   // kept for the back substitution
+        }
+    }
+    wave_lds_sync();
+    if (lane < 32) {                                // y_k = X r_k, in place of r_k
+        double y = 0.0;
+#pragma unroll
+        for (int j = 0; j < TB; ++j) y = __builtin_fma(-li[felem(lane, j)], Lr[j], y);
+        quad += y * y;
+        Lr[lane] = y;
+    }
+    return FactorAcc{quad, dpr, pexp};
+}
+
+template <int NW, int MAXR, bool COND>   // MAXR tile rows per row-owning wave: nt <= MAXR * (NW - 1)
 __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     constexpr int NT = 64 * NW;
     extern __shared__ double smem64[];
@@ -123,9 +214,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     double *Lr = Lt + npad;           // [npad] rhs r, reduced in place; segment k becomes y_k (then alpha_k)
     double *Ldia = Lr + npad;         // [npad] velerr^2 + jit^2 (padding: 1)
     double *fb = Ldia + npad;         // [TB][FS] the factor's row buffer; back substitution partial sums
-    double *li = fb + TB * FS;        // [TB][FS] -X = -L_kk^-1 of the step, fragment layout (first TILE);
-                                      //          the inverse's columns while the factor runs
-    double *red = li + TB * FS;       // [2 NW]
+    double *li = fb + TB * FS;        // [TILE] -X = -L_kk^-1 of the step, fragment layout
+    double *red = li + TILE;          // [2 NW]
     SC *tab = reinterpret_cast<SC *>(red + 2 * NW);
     PlanetK *pks = reinterpret_cast<PlanetK *>(tab + kTabN);
     int *oks = reinterpret_cast<int *>(pks + RVK_MAX_PLANETS);
@@ -203,182 +293,144 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     }
             }
         };
-        double quad = 0.0;          // sum of y^2 over this wave's lanes
-        double dpr = 1.0;           // product of this wave's pivots L_ii^2, renormalised (x 2^pexp)
+        double quad = 0.0;          // sum of y^2 (the factor wave's lanes)
+        double dpr = 1.0;           // product of the pivots L_ii^2, renormalised (x 2^pexp; factor wave)
         int pexp = 0;
-        Acc nacc[MAXR], dacc;
+        // Waves 0 .. NA-1 own the tile rows (wr, wr + NA, ...) and do the MFMA work; wave NA
+        // factors every diagonal tile.  The roles run separate loops with the same barriers,
+        // so the factor's registers (a 32-double row per lane) never coexist with the
+        // accumulators.  acc(k, k) travels to the factor wave through fb.
+        constexpr int NA = NW - 1;
+        auto put_diag = [&](const Acc &A) {          // fb[row][col] = acc(k, k) (from -acc^T, C/D layout)
 #pragma unroll
-        for (int q = 0; q < MAXR; ++q) {
-            const int bi = wr + NW * q;
-            if (bi < nt) {
-                Acc t;
-                cov_tile(bi, 0, t);
-                if (bi == 0) dacc = t;
-                else park(wk + tix(bi, 0) * TILE, t, lane);
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        fb[(16 * q + (lane & 15)) * FS + 16 * p + (lane >> 4) + 4 * i] = -A.c[p][q][i];
+        };
+        if (wr < NA) {
+#pragma unroll
+            for (int q = 0; q < MAXR; ++q) {
+                const int bi = wr + NA * q;
+                if (bi < nt) {
+                    Acc t;
+                    cov_tile(bi, 0, t);
+                    if (bi == 0) put_diag(t);
+                    else park(wk + tix(bi, 0) * TILE, t, lane);
+                }
             }
         }
         __syncthreads();
-        for (int k = 0; k < nt; ++k) {
-            // ---- P(k): factor the diagonal tile (the owner of row k) ---------------------------
-            if (wr == k % NW) {
+        if (wr == NA) {
+            // ---- the factor wave: P(k) for every k, then the step's barriers ----------------------
+            for (int k = 0; k < nt; ++k) {
+                G64_MARK(k, 0);
                 __builtin_amdgcn_s_setprio(1);    // the step's critical path goes first on its SIMD
-#pragma unroll
-                for (int p = 0; p < 2; ++p)
-#pragma unroll
-                    for (int q = 0; q < 2; ++q)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            fb[(16 * q + (lane & 15)) * FS + 16 * p + (lane >> 4) + 4 * i] = -dacc.c[p][q][i];
-                wave_lds_sync();
-                // lane i < 32 works on row i of acc(k, k) (fb, in place: it becomes row i of L_kk);
-                // lane 32 + j on column j of the identity (xb), which becomes column j of
-                // X = L_kk^-1 under the same updates (forward substitution).  Dynamic loops over
-                // LDS-resident vectors: the factor needs few registers, so nothing else has to
-                // leave them while it runs.
-                double *xb = li;   // li is free until the end of the factor (S1(k-1) read it before B2)
-                if (lane >= 32)
-                    for (int m = 0; m < TB; ++m) xb[m * FS + (lane - 32)] = m == lane - 32 ? 1.0 : 0.0;
-                wave_lds_sync();
-                double *vec = lane < 32 ? fb + lane * FS : xb + (lane - 32);
-                const int vs = lane < 32 ? 1 : FS;
-#pragma unroll 1
-                for (int r = 0; r < TB; ++r) {
-                    const int rr = __builtin_amdgcn_readfirstlane(r);
-                    const double *lrow = fb + rr * FS;           // row r of L (L[r][m], m < r: final)
-                    double v0 = vec[rr * vs], v1 = 0.0;
-                    int m = 0;
-#pragma unroll 1
-                    for (; m + 1 < rr; m += 2) {
-                        const double2 l2 = *reinterpret_cast<const double2 *>(lrow + m);
-                        v0 = __builtin_fma(-vec[m * vs], l2.x, v0);
-                        v1 = __builtin_fma(-vec[(m + 1) * vs], l2.y, v1);
-                    }
-                    if (m < rr) v0 = __builtin_fma(-vec[m * vs], lrow[m], v0);
-                    const double v = v0 + v1;
-                    const double piv = readlane_d(v, rr);        // L[r][r]^2 (<= 0 / NaN propagate)
-                    const double dd = __builtin_sqrt(piv);
-                    const double inv = 1.0 / dd;
-                    wave_lds_sync();                             // every lane has read row r
-                    vec[rr * vs] = lane == rr ? dd : v * inv;
-                    wave_lds_sync();
-                    dpr *= piv;
-                    if ((r & 7) == 7) {
-                        int e;
-                        dpr = __builtin_frexp(dpr, &e);
-                        pexp += e;
-                    }
-                }
-                double av[TB];
-                if (lane >= 32)
-#pragma unroll
-                    for (int r = 0; r < TB; ++r) av[r] = xb[r * FS + (lane - 32)];
-                wave_lds_sync();
-                if (lane >= 32) {                               // -X, fragment layout
-                    const int j = lane - 32, kk = j >> 2;
-#pragma unroll
-                    for (int r = 0; r < TB; ++r) {
-                        const int o = fpair(r >> 4, kk >> 1, (j & 3) * 16 + (r & 15)) + (kk & 1);
-                        li[o] = -av[r];
-                        if (COND) wk[tix(k, k) * TILE + o] = -av[r];   // kept for the back substitution
-                    }
-                }
-                wave_lds_sync();
-                if (lane < 32) {                                // y_k = X r_k, in place of r_k
-                    double y = 0.0;
-#pragma unroll
-                    for (int j = 0; j < TB; ++j) y = __builtin_fma(-li[felem(lane, j)], Lr[k * TB + j], y);
-                    quad += y * y;
-                    Lr[k * TB + lane] = y;
+                {
+                    const FactorAcc fa = factor_diag((lds_d *)fb, (lds_d *)li, (lds_d *)(Lr + k * TB),
+                                                     COND ? wk + tix(k, k) * TILE : nullptr, FactorAcc{quad, dpr, pexp});
+                    quad = fa.quad;
+                    dpr = fa.dpr;
+                    pexp = fa.pexp;
                 }
                 __builtin_amdgcn_s_setprio(0);
+                G64_MARK(k, 1);
+                G64_MARK(k, 2);
+                __syncthreads();                            // B1: -X and y_k published
+                G64_MARK(k, 3);
+                if (k + 1 == nt) break;
+                G64_MARK(k, 4);
+                __syncthreads();                            // B2 (S1 runs on the other waves)
+                G64_MARK(k, 5);
+                __syncthreads();                            // B3: acc(k+1, k+1) in fb
+                G64_MARK(k, 6);
             }
+        } else {
+            // ---- the row owners: the next column's accumulation, S1, S2 --------------------------
+            Acc nacc[MAXR];
+            for (int k = 0; k < nt; ++k) {
+                G64_MARK(k, 0);
+                G64_MARK(k, 1);
+                if (k + 1 < nt) {
 #pragma unroll
-            for (int p = 0; p < 2; ++p)     // (dacc is dead until S2 sets it again)
+                    for (int q = 0; q < MAXR; ++q) {
+                        const int bi = wr + NA * q;
+                        if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
+                    }
+                    // operands: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows at a time,
+                    // a quarter tile (2 of the 8 k-steps) per register set; sets X / Y alternate so the
+                    // next quarter's loads are in flight during this quarter's MFMAs.  The trip past the
+                    // end re-reads the last quarter (unconditional loads, exact waits).
+                    auto pass = [&](auto q0c) {
+                        constexpr int Q0 = decltype(q0c)::value;
+                        constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
+                        bool any = false;
 #pragma unroll
-                for (int qq = 0; qq < 2; ++qq) dacc.c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
-            // every accumulator is (re)defined here, after the factor: none is live across it
-#pragma unroll
-            for (int q = 0; q < MAXR; ++q)
-#pragma unroll
-                for (int p = 0; p < 2; ++p)
-#pragma unroll
-                    for (int qq = 0; qq < 2; ++qq) nacc[q].c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
-            // ---- P(k): the next column's tiles, all but the j = k term --------------------------
-            if (k + 1 < nt) {
-#pragma unroll
-                for (int q = 0; q < MAXR; ++q) {
-                    const int bi = wr + NW * q;
-                    if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
-                }
-                // operands: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows at a time,
-                // half a tile (4 of the 8 k-steps) per register set; sets X / Y alternate so the next
-                // half's loads are in flight during this half's MFMAs.  The trip past the end re-reads
-                // the last half (unconditional loads, exact waits).
-                auto pass = [&](auto q0c) {
-                    constexpr int Q0 = decltype(q0c)::value;
-                    constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
-                    bool any = false;
-#pragma unroll
-                    for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NW * q >= k + 1) && (wr + NW * q < nt);
-                    if (!any || k == 0) return;
-                    struct Ops {
-                        double2 a[2][2], b[R][2][2];
-                    };
-                    auto issue = [&](Ops &o, int hx) {
-                        const int hh = hx < 2 * k ? hx : 2 * k - 1;
-                        const int j = hh >> 1, half = hh & 1;
-                        const double2 *ta = reinterpret_cast<const double2 *>(wk + tix(k + 1, j) * TILE);
-#pragma unroll
-                        for (int s = 0; s < 2; ++s)
-#pragma unroll
-                            for (int u = 0; u < 2; ++u) o.a[s][u] = ta[(s * 4 + 2 * half + u) * 64 + lane];
-#pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const int bi = wr + NW * (Q0 + r);
-                            const bool live = bi >= k + 1 && bi < nt;
-                            const double2 *tb = reinterpret_cast<const double2 *>(wk + tix(live ? bi : k + 1, j) * TILE);
+                        for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NA * q >= k + 1) && (wr + NA * q < nt);
+                        if (!any || k == 0) return;
+                        constexpr int KP = 1, NSET = 4 / KP;   // fragment pairs per register set, sets per tile
+                        struct Ops {
+                            double2 a[2][KP], b[R][2][KP];
+                        };
+                        auto issue = [&](Ops &o, int hx) {
+                            const int hh = hx < NSET * k ? hx : NSET * k - 1;
+                            const int j = hh / NSET, part = hh % NSET;
+                            const double2 *ta = reinterpret_cast<const double2 *>(wk + tix(k + 1, j) * TILE);
 #pragma unroll
                             for (int s = 0; s < 2; ++s)
 #pragma unroll
-                                for (int u = 0; u < 2; ++u) o.b[r][s][u] = tb[(s * 4 + 2 * half + u) * 64 + lane];
-                        }
-                    };
-                    auto consume = [&](const Ops &o) {
+                                for (int u = 0; u < KP; ++u) o.a[s][u] = ta[(s * 4 + KP * part + u) * 64 + lane];
 #pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const int bi = wr + NW * (Q0 + r);
-                            if (bi >= k + 1 && bi < nt) {
-                                Acc &acc = nacc[Q0 + r];
+                            for (int r = 0; r < R; ++r) {
+                                const int bi = wr + NA * (Q0 + r);
+                                const bool live = bi >= k + 1 && bi < nt;
+                                const double2 *tb = reinterpret_cast<const double2 *>(wk + tix(live ? bi : k + 1, j) * TILE);
 #pragma unroll
-                                for (int u = 0; u < 2; ++u)
+                                for (int s = 0; s < 2; ++s)
 #pragma unroll
-                                    for (int cmp = 0; cmp < 2; ++cmp)
-#pragma unroll
-                                        for (int p = 0; p < 2; ++p)
-#pragma unroll
-                                            for (int q = 0; q < 2; ++q)
-                                                acc.c[p][q] = mfma64(cmp ? o.a[p][u].y : o.a[p][u].x,
-                                                                     cmp ? o.b[r][q][u].y : o.b[r][q][u].x, acc.c[p][q]);
+                                    for (int u = 0; u < KP; ++u) o.b[r][s][u] = tb[(s * 4 + KP * part + u) * 64 + lane];
                             }
+                        };
+                        auto consume = [&](const Ops &o) {
+#pragma unroll
+                            for (int r = 0; r < R; ++r) {
+                                const int bi = wr + NA * (Q0 + r);
+                                if (bi >= k + 1 && bi < nt) {
+                                    Acc &acc = nacc[Q0 + r];
+#pragma unroll
+                                    for (int u = 0; u < KP; ++u)
+#pragma unroll
+                                        for (int cmp = 0; cmp < 2; ++cmp)
+#pragma unroll
+                                            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                                                for (int q = 0; q < 2; ++q)
+                                                    acc.c[p][q] = mfma64(cmp ? o.a[p][u].y : o.a[p][u].x,
+                                                                         cmp ? o.b[r][q][u].y : o.b[r][q][u].x, acc.c[p][q]);
+                                }
+                            }
+                        };
+                        Ops X, Y;
+                        issue(X, 0);
+                        for (int hx = 0; hx < NSET * k; hx += 2) {
+                            issue(Y, hx + 1);
+                            consume(X);
+                            issue(X, hx + 2);
+                            consume(Y);
                         }
                     };
-                    Ops X, Y;
-                    issue(X, 0);
-                    for (int hx = 0; hx < 2 * k; hx += 2) {
-                        issue(Y, hx + 1);
-                        consume(X);
-                        issue(X, hx + 2);
-                        consume(Y);
-                    }
-                };
-                pass(std::integral_constant<int, 0>{});
-                if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
-                if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
-                if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
-            }
-            __syncthreads();                                // B1: -X and y_k published
-            if (k + 1 == nt) break;
-            // ---- S1(k): L(bi, k) = acc(bi, k) X^T, stored; rhs update --------------------------
+                    pass(std::integral_constant<int, 0>{});
+                    if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
+                    if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
+                    if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
+                }
+                G64_MARK(k, 2);
+                __syncthreads();                            // B1: -X and y_k published
+                G64_MARK(k, 3);
+                if (k + 1 == nt) break;
+                // ---- S1(k): L(bi, k) = acc(bi, k) X^T, stored; rhs update ----------------------
             {
                 double xa[2][8];
                 {
@@ -399,7 +451,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     for (int i = 0; i < 4; ++i) yv[p][i] = Lr[k * TB + 16 * p + (lane >> 4) + 4 * i];
 #pragma unroll
                 for (int q = 0; q < MAXR; ++q) {
-                    const int bi = wr + NW * q;
+                    const int bi = wr + NA * q;
                     if (bi > k && bi < nt) {
                         double *T = wk + tix(bi, k) * TILE;
                         Acc cur;
@@ -438,16 +490,16 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     }
                 }
             }
-            __syncthreads();                                // B2: L(k+1, k) published
-            // ---- S2(k): the j = k term; park for S1(k+1) ---------------------------------------
-            // (L(bi, k) is re-read from the workspace -- an L1/L2 hit -- rather than kept in
-            // registers from S1, which would not fit next to the accumulators)
+                G64_MARK(k, 4);
+                __syncthreads();                            // B2: L(k+1, k) published
+                G64_MARK(k, 5);
+                // ---- S2(k): the j = k term; park for S1(k+1), the diagonal tile to fb -----------
             {
                 double af[2][8];
                 load_frags(wk + tix(k + 1, k) * TILE, af, lane);
 #pragma unroll
                 for (int q = 0; q < MAXR; ++q) {
-                    const int bi = wr + NW * q;
+                    const int bi = wr + NA * q;
                     if (bi > k && bi < nt) {
                         double bf[2][8];
                         load_frags(wk + tix(bi, k) * TILE, bf, lane);
@@ -458,10 +510,13 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                                 for (int qq = 0; qq < 2; ++qq)
                                     nacc[q].c[p][qq] = mfma64(af[p][kk], bf[qq][kk], nacc[q].c[p][qq]);
-                        if (bi == k + 1) dacc = nacc[q];
+                        if (bi == k + 1) put_diag(nacc[q]);
                         else park(wk + tix(bi, k + 1) * TILE, nacc[q], lane);
                     }
                 }
+            }
+                __syncthreads();                            // B3: acc(k+1, k+1) in fb
+                G64_MARK(k, 6);
             }
         }
         if (!COND) {
@@ -542,12 +597,12 @@ namespace rvk {
 
 Gp64Shape gp64_shape(int n) {
     const int nt = (n + TB - 1) / TB;
-    return nt <= 16 ? Gp64Shape{8, 2} : Gp64Shape{8, 4};
+    return nt <= 16 ? Gp64Shape{8, 3} : Gp64Shape{8, 5};   // 7 row-owning waves + the factor wave
 }
 
 size_t gp64_lds_bytes(int n, int nw) {
     const int nt = (n + TB - 1) / TB;
-    size_t b = sizeof(double) * (3 * (size_t)nt * TB + 2 * TB * FS + 2 * (size_t)nw);
+    size_t b = sizeof(double) * (3 * (size_t)nt * TB + TB * FS + TILE + 2 * (size_t)nw);
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
     return b;
 }
@@ -561,8 +616,14 @@ gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape s
     (void)multi;
     (void)tp;
     if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
-    if (sh.maxr == 2) return condition ? launch_gp64<8, 2, true> : launch_gp64<8, 2, false>;
-    return condition ? launch_gp64<8, 4, true> : launch_gp64<8, 4, false>;
+    if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true> : launch_gp64<8, 3, false>;
+    return condition ? launch_gp64<8, 5, true> : launch_gp64<8, 5, false>;
 }
 
 }  // namespace rvk
+
+#if RVK_GP64_TRACE
+extern "C" int rvk_gp64_trace_dump(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gp64_trace), sizeof(g_gp64_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
