@@ -162,6 +162,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     struct Fetch {
         Draw dr;
         double z, a, b, lpo;
+        long long nacc;    // the walker's acceptance count (read here, written +1 at the tail)
     };
     auto fetch = [&](long long w) {
         Fetch f;
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const double zt = (run.a - 1.0) * f.dr.zu + 1.0;
         f.z = zt * zt / run.a;
         f.lpo = run.lp[f.dr.s];
+        f.nacc = run.nacc ? run.nacc[f.dr.s] : 0;
         f.a = f.b = 0.0;
         if (lane < D) {
             f.a = run.x[f.dr.s * D + lane];
@@ -216,8 +218,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             double lpw = FUSE ? 0.0 : (post.lp ? post.lp[w] : 0.0);
             // SAMPLE: the accept test's operands are loaded before the epoch loop, so their latency
             // (sidx -> lp[sidx] is a dependent pair) hides under the loop instead of the wave's tail
-            long long sw_s = 0;
-            double lp_old_s = 0.0, fac_s = 0.0, au_s = 1.0;
+            long long sw_s = 0, nacc_s = 0;
+            double lp_old_s = 0.0, fac_s = 0.0, au_s = 1.0, lau_s = 0.0;
             if constexpr (FUSE) {   // this wave's proposal (StretchMove.get_proposal + fit.py:3461-3482)
                 const PostDev &pd = sa.pd;
                 const int D = pd.n_free;
@@ -256,7 +258,9 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 lpw = dead ? -INFINITY : lp;
                 fac_s = ((double)D - 1.0) * log(z);
                 au_s = dr.au;
+                lau_s = log(au_s);                        // off the wave's tail
                 sw_s = dr.s;
+                nacc_s = f.nacc;
                 LL_MARK(2);
             } else if constexpr (SAMPLE != 0) {
                 sw_s = sa.sidx[w];
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 const int D = sa.D;
                 const long long sw = sw_s;
                 const double lp_old = lp_old_s;
-                const bool acc = fac_s + res - lp_old > log(au_s);
+                const bool acc = fac_s + res - lp_old > (FUSE ? lau_s : log(au_s));
                 double *xs = run.x + sw * D;
                 const double *qw = FUSE ? fq[j] : sa.q + w * D;
                 const long long W2 = 2 * n_walkers;
@@ -390,7 +394,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 if (lane == 0) {
                     if (acc) {
                         run.lp[sw] = res;
-                        if (run.nacc) run.nacc[sw] += 1;
+                        if (run.nacc) run.nacc[sw] = (FUSE ? nacc_s : run.nacc[sw]) + 1;
                     }
                     if (run.lnpc) run.lnpc[(long long)sa.step * W2 + sw] = acc ? res : lp_old;
                 }
