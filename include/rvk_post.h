@@ -106,6 +106,17 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t n_walkers, i
                     double *d_chain, double *d_lnp, int64_t *d_naccepted, int32_t *d_status,
                     void *stream);
 
+/* One half-step of the same stretch move over a SLICE of the active half's proposals
+ * [j0, j0 + count) -- the multi-GPU form (ravest_amd.distributed.ShardedDeviceSampler): every
+ * rank holds the whole state, makes and evaluates its slice of the proposals (Philox draws
+ * keyed by the global proposal index and `step` = step0 + step, so the union over ranks is
+ * the single-GPU half-step bit for bit), updates those walkers in d_x / d_lp and counts their
+ * acceptances; the caller all-gathers the updated rows before the next half-step.  No chain
+ * is written here.  Stream-ordered. */
+int rvk_stretch_half(rvk_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t half, int64_t j0,
+                     int64_t count, double a, uint64_t seed, uint64_t step, int64_t *d_naccepted,
+                     int32_t *d_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         Fetch f;
         const RunArgs &run = *sa.run;
         const int D = sa.pd.n_free;
-        f.dr = draw(run, sa.step, sa.half, w, n_walkers);
+        f.dr = draw(run, sa.step, sa.half, sa.j0 + w, sa.hfull);   // global proposal index within the half
         const double zt = (run.a - 1.0) * f.dr.zu + 1.0;
         f.z = zt * zt / run.a;
         f.lpo = run.lp[f.dr.s];
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 const bool acc = fac_s + res - lp_old > (FUSE ? lau_s : log(au_s));
                 double *xs = run.x + sw * D;
                 const double *qw = FUSE ? fq[j] : sa.q + w * D;
-                const long long W2 = 2 * n_walkers;
+                const long long W2 = 2 * sa.hfull;
                 double *chain = run.chain ? run.chain + (long long)sa.step * W2 * D : nullptr;
                 if (lane == 0 && isnan(res)) atomicOr(run.status, 1);
                 for (int c = lane; c < D; c += 64) {

@@ -43,7 +43,8 @@ __global__ __launch_bounds__(256) void logprior_kernel(PostDev pd, const double 
 // then its full row and log-prior.  The accept / reject runs in the epilogue of the
 // log-likelihood kernel (SAMPLE mode) or in accept_kernel.
 __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs *__restrict__ runp, int step,
-                                                      int half, long long H, double *__restrict__ q,
+                                                      int half, long long H, long long j0, long long hfull,
+                                                      double *__restrict__ q,
                                                       double *__restrict__ full,
                                                       double *__restrict__ lp, double *__restrict__ fac,
                                                       double *__restrict__ au, long long *__restrict__ sidx) {
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs 
     const double *x = run.x, a = run.a;
     const RowPre pre = row_pre(pd);
     for (long long j = (long long)blockIdx.x * kWavesPerBlock + wv; j < H; j += (long long)gridDim.x * kWavesPerBlock) {
-        const Draw d = draw(run, step, half, j, H);
+        const Draw d = draw(run, step, half, j0 + j, hfull);   // proposal j0 + j of the half
         const double zt = (a - 1.0) * d.zu + 1.0;
         const double z = zt * zt / a;
         const double *xs = x + d.s * D, *xc = x + d.c * D;
@@ -115,32 +116,38 @@ struct rvk_post {
     }
 };
 
-// Kernels of n steps reading this chunk's RunArgs (p->d_run): propose, then the
-// likelihood with the accept / reject fused in (production solver) or the
-// likelihood and accept_kernel (reference solver).
-static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
+// Kernels of one half-step over proposals [j0, j0 + count) of a half of hfull walkers, reading
+// this chunk's RunArgs (p->d_run): propose, then the likelihood with the accept / reject fused in
+// (production solver), or both in one kernel (fused path), or the likelihood and accept_kernel
+// (reference solver).
+static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long j0, long long count,
+                         long long hfull) {
     rvk_handle *h = p->h;
     const PostDev pd = p->dev();
     const PostArgs post{p->d_lp, p->jac, p->renorm};
     const bool fused = p->fusable && h->solver == 0 && h->sample_fused;
+    const long long H = count;
+    if (fused) {
+        const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, hfull};
+        h->sample_fused(st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
+        return;
+    }
+    hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, s, half, H, j0, hfull,
+                       p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
+    if (h->solver == 0 && h->sample) {
+        const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s, half, pd, j0, hfull};
+        h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
+    } else {
+        h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
+        hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, p->d_run, s, H, p->n_free,
+                           p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_nlp);
+    }
+}
+
+// Kernels of n steps (both halves, all proposals) reading this chunk's RunArgs.
+static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
     for (int s = 0; s < n; ++s)
-        for (int half = 0; half < 2; ++half) {
-            if (fused) {   // one kernel per half-step: proposals in the likelihood kernel's prep
-                const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd};
-                h->sample_fused(st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
-                continue;
-            }
-            hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, s, half, H,
-                               p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
-            if (h->solver == 0 && h->sample) {
-                const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s, half, pd};
-                h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
-            } else {
-                h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
-                hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, p->d_run, s, H, p->n_free,
-                                   p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_nlp);
-            }
-        }
+        for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H);
 }
 
 // The kStepsPerGraph-step chunk as a HIP graph, captured once per (H, solver) and
@@ -372,6 +379,29 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
             enqueue_steps(p, st, H, n);
         }
     }
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_stretch_half(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t half, int64_t j0, int64_t count,
+                     double a, uint64_t seed, uint64_t step, int64_t *d_naccepted, int32_t *d_status, void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL posterior");
+    if (W < 4 || (W & 1)) return fail(RVK_E_ARG, "n_walkers must be even and >= 4");
+    if (half != 0 && half != 1) return fail(RVK_E_ARG, "half must be 0 or 1");
+    const long long H = W / 2;
+    if (j0 < 0 || count < 0 || j0 + count > H) return fail(RVK_E_ARG, "proposal slice outside the half");
+    if (!(a > 1.0)) return fail(RVK_E_ARG, "stretch scale a must be > 1");
+    if (!d_x || !d_lp || !d_status) return fail(RVK_E_ARG, "NULL device buffer");
+    if (count == 0) return RVK_OK;
+    int rc = reserve_impl(p, count);
+    if (rc) return rc;
+    rvk_handle *h = p->h;
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(h->device));
+    const RunArgs run{d_x, d_lp, (long long *)d_naccepted, (int *)d_status, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, nullptr, seed, step, a};
+    hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+    enqueue_half(p, st, 0, half, j0, count, H);
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

@@ -267,6 +267,8 @@ struct SampleArgs {
     int step;                   // step within the chunk
     int half;                   // active half (fused proposals, SAMPLE == 2)
     PostDev pd;                 // the posterior (fused proposals, SAMPLE == 2)
+    long long j0;               // the launch's proposals are j0 .. j0 + count - 1 of the half
+    long long hfull;            // walkers per half (the complement's range; chain row stride / 2)
 };
 
 // Limits of the fused proposal path (loglike_kernel SAMPLE == 2): the proposal, its full row
