@@ -138,7 +138,6 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     __shared__ int fcol[FP];
     __shared__ double ftm[FP];
     __shared__ PriorSlot fsl[FS];
-    __shared__ double fterm[FUSE ? BLK / 64 : 1][FS];
     const int lane = threadIdx.x & 63;
     // Epoch data does not depend on the walker: this lane's first epoch is loaded once,
     // before anything else, so its latency hides under the table fill and the prep.
@@ -162,6 +161,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     struct Fetch {
         Draw dr;
         double z, a, b, lpo;
+        double fac, lau;   // (D - 1) log z and log u': the draws' logs, off the prep's chain
         long long nacc;    // the walker's acceptance count (read here, written +1 at the tail)
     };
     auto fetch = [&](long long w) {
@@ -178,6 +178,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             f.a = run.x[f.dr.s * D + lane];
             f.b = run.x[f.dr.c * D + lane];
         }
+        f.fac = ((double)D - 1.0) * log(f.z);
+        f.lau = log(f.dr.au);
         return f;
     };
     Fetch pre{};
@@ -221,46 +223,58 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             long long sw_s = 0, nacc_s = 0;
             double lp_old_s = 0.0, fac_s = 0.0, au_s = 1.0, lau_s = 0.0;
             if constexpr (FUSE) {   // this wave's proposal (StretchMove.get_proposal + fit.py:3461-3482)
+                // Lane-parallel and register-resident: lane c < D holds q_c, lane k < p_full the
+                // full row's column k (a ds_bpermute of q), lane k < n_prior its prior term; only
+                // the planet constants and the row go through LDS, for the epoch loop.
                 const PostDev &pd = sa.pd;
                 const int D = pd.n_free;
                 const Fetch f = (base == (long long)blockIdx.x * wb && j == wv) ? pre : fetch(w);
-                const Draw dr = f.dr;
-                const double z = f.z;
                 lp_old_s = f.lpo;                         // (needed only in the epilogue)
-                if (lane < D) {
-                    fq[j][lane] = f.b - (f.b - f.a) * z;
+                const double q_s = lane < D ? f.b - (f.b - f.a) * f.z : 0.0;
+                if (lane < D) {                           // parked for the epilogue (read back by the same lane)
+                    fq[j][lane] = q_s;
                     fx[j][lane] = f.a;
                 }
-                wave_lds_sync();
+                const int fc = lane < pd.p_full ? fcol[lane] : 0;
+                double fv = shfl_d(q_s, fc < 0 ? 0 : fc);
                 if (lane < pd.p_full) {
-                    const int f = fcol[lane];
-                    ff[j][lane] = f >= 0 ? fq[j][f] : ftm[lane];
+                    if (fc < 0) fv = ftm[lane];
+                    ff[j][lane] = fv;
                 }
-                wave_lds_sync();
-                bool dead = false;
-                if (lane < pd.n_inst) dead = ff[j][5 * pd.n_planets + pd.n_inst + lane] < 0.0;   // fit.py:3465-3468
-                if (lane < pd.n_prior) {
-                    const PriorSlot &sl = fsl[lane];
-                    fterm[wv][lane] = prior_lp_basic(sl.kind, sl.p, ff[j][sl.src]);
+                const int ioff = 5 * pd.n_planets + pd.n_inst;
+                const double jv = shfl_d(fv, ioff + (lane < pd.n_inst ? lane : 0));
+                const bool dead0 = lane < pd.n_inst && jv < 0.0;                              // fit.py:3465-3468
+                double term = 0.0;
+                {
+                    const int src = lane < pd.n_prior ? fsl[lane].src : 0;
+                    const double xv = shfl_d(fv, src);
+                    if (lane < pd.n_prior) {
+                        const PriorSlot &sl = fsl[lane];
+                        term = prior_lp_basic(sl.kind, sl.p, xv);
+                    }
                 }
-                if (lane < NP) {
-                    PlanetK pk;
-                    const double *p5 = ff[j] + 5 * lane;
-                    const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
-                    pks[j][lane] = pk;
-                    okp[j][lane] = ok;
+                {
+                    const int pl = lane < NP ? lane : 0;
+                    double p5[5];
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) p5[k] = shfl_d(fv, 5 * pl + k);
+                    if (lane < NP) {
+                        PlanetK pk;
+                        const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
+                        pks[j][lane] = pk;
+                        okp[j][lane] = ok;
+                    }
                 }
-                wave_lds_sync();
-                dead = __builtin_amdgcn_ballot_w64(dead) != 0;
+                bool dead = __builtin_amdgcn_ballot_w64(dead0) != 0;
                 double lp = 0.0;
-                for (int k = 0; k < pd.n_prior; ++k) lp += fterm[wv][k];                      // the reference's key order
+                for (int k = 0; k < pd.n_prior; ++k) lp += readlane_d(term, k);            // the reference's key order
                 if (!isfinite(lp)) dead = true;                                                // fit.py:3481-3482
                 lpw = dead ? -INFINITY : lp;
-                fac_s = ((double)D - 1.0) * log(z);
-                au_s = dr.au;
-                lau_s = log(au_s);                        // off the wave's tail
-                sw_s = dr.s;
+                fac_s = f.fac;
+                lau_s = f.lau;
+                sw_s = f.dr.s;
                 nacc_s = f.nacc;
+                wave_lds_sync();                          // pks / ff of this walker, for the epoch loop
                 LL_MARK(2);
             } else if constexpr (SAMPLE != 0) {
                 sw_s = sa.sidx[w];
@@ -382,14 +396,22 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 const double lp_old = lp_old_s;
                 const bool acc = fac_s + res - lp_old > (FUSE ? lau_s : log(au_s));
                 double *xs = run.x + sw * D;
-                const double *qw = FUSE ? fq[j] : sa.q + w * D;
                 const long long W2 = 2 * sa.hfull;
                 double *chain = run.chain ? run.chain + (long long)sa.step * W2 * D : nullptr;
                 if (lane == 0 && isnan(res)) atomicOr(run.status, 1);
+                if constexpr (FUSE) {             // D <= kFuseMaxD < 64: lane c holds coordinate c
+                    if (lane < D) {
+                        const double v = acc ? fq[j][lane] : fx[j][lane];
+                        if (acc) xs[lane] = v;
+                        if (chain) chain[sw * D + lane] = v;
+                    }
+                } else {
+                const double *qw = sa.q + w * D;
                 for (int c = lane; c < D; c += 64) {
-                    const double v = acc ? qw[c] : (FUSE ? fx[j][c] : xs[c]);
+                    const double v = acc ? qw[c] : xs[c];
                     if (acc) xs[c] = v;
                     if (chain) chain[sw * D + c] = v;
+                }
                 }
                 if (lane == 0) {
                     if (acc) {

@@ -521,6 +521,15 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+// v from lane `src` (0..63) of this wave, per lane (two ds_bpermute_b32; no LDS allocation)
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int addr = src << 2;
+    const unsigned lo = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)b);
+    const unsigned hi = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(b >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 // ln(m * 2^k) for a frexp mantissa m in [0.5, 1): fdlibm e_log.c's reduction and
 // kernel (m -> [sqrt(1/2), sqrt(2)), s = f / (2 + f), degree-14 polynomial in s),
 // ~1 ulp, about a quarter of the generic log's instructions.  Callers route
