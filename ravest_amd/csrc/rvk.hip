@@ -267,7 +267,12 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 }
                 bool dead = __builtin_amdgcn_ballot_w64(dead0) != 0;
                 double lp = 0.0;
-                for (int k = 0; k < pd.n_prior; ++k) lp += readlane_d(term, k);            // the reference's key order
+                // the reference's key order; lanes >= n_prior hold +0.0, and lp (from +0.0) is never
+                // -0.0, so the padding to a multiple of 8 adds exactly nothing
+                for (int k0 = 0; k0 < pd.n_prior; k0 += 8) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) lp += readlane_d(term, k0 + k);
+                }
                 if (!isfinite(lp)) dead = true;                                                // fit.py:3481-3482
                 lpw = dead ? -INFINITY : lp;
                 fac_s = f.fac;
