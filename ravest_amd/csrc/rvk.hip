@@ -159,7 +159,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     // fill; the posterior's constants are staged in LDS (each is read in a loop with a runtime
     // trip count: from global memory every iteration would wait on a load).
     struct Fetch {
-        Draw dr;
+        long long s, c;    // the walker and its complement
         double z, a, b, lpo;
         double fac, lau;   // (D - 1) log z and log u': the draws' logs, off the prep's chain
         long long nacc;    // the walker's acceptance count (read here, written +1 at the tail)
@@ -168,18 +168,21 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         Fetch f;
         const RunArgs &run = *sa.run;
         const int D = sa.pd.n_free;
-        f.dr = draw(run, sa.step, sa.half, sa.j0 + w, sa.hfull);   // global proposal index within the half
-        const double zt = (run.a - 1.0) * f.dr.zu + 1.0;
-        f.z = zt * zt / run.a;
-        f.lpo = run.lp[f.dr.s];
-        f.nacc = run.nacc ? run.nacc[f.dr.s] : 0;
+        const long long j = sa.j0 + w;   // global proposal index within the half
+        const PreDraw p = sa.pre ? sa.pre[((long long)sa.step * 2 + sa.half) * sa.hfull + j]
+                                 : make_pre(run, sa.step, sa.half, j, sa.hfull, D);
+        f.s = p.s;
+        f.c = p.c;
+        f.z = p.z;
+        f.fac = p.fac;
+        f.lau = p.lau;
+        f.lpo = run.lp[p.s];
+        f.nacc = run.nacc ? run.nacc[p.s] : 0;
         f.a = f.b = 0.0;
         if (lane < D) {
-            f.a = run.x[f.dr.s * D + lane];
-            f.b = run.x[f.dr.c * D + lane];
+            f.a = run.x[p.s * D + lane];
+            f.b = run.x[p.c * D + lane];
         }
-        f.fac = ((double)D - 1.0) * log(f.z);
-        f.lau = log(f.dr.au);
         return f;
     };
     Fetch pre{};
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 lpw = dead ? -INFINITY : lp;
                 fac_s = f.fac;
                 lau_s = f.lau;
-                sw_s = f.dr.s;
+                sw_s = f.s;
                 nacc_s = f.nacc;
                 wave_lds_sync();                          // pks / ff of this walker, for the epoch loop
                 LL_MARK(2);

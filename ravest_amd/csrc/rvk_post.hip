@@ -103,6 +103,7 @@ struct rvk_post {
     double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_au = nullptr;
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;              // rvk_stretch_run's per-chunk arguments
+    PreDraw *d_pre = nullptr;              // [kStepsPerGraph][2][capw] the chunk's draws (fused path)
     double *d_xin = nullptr, *d_oin = nullptr;   // rvk_logpost's host-buffer staging, grown on demand
     size_t cap_xin = 0, cap_oin = 0;
     hipStream_t cap = nullptr;             // capture stream
@@ -121,21 +122,21 @@ struct rvk_post {
 // (production solver), or both in one kernel (fused path), or the likelihood and accept_kernel
 // (reference solver).
 static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long j0, long long count,
-                         long long hfull) {
+                         long long hfull, const PreDraw *pre) {
     rvk_handle *h = p->h;
     const PostDev pd = p->dev();
     const PostArgs post{p->d_lp, p->jac, p->renorm};
     const bool fused = p->fusable && h->solver == 0 && h->sample_fused;
     const long long H = count;
     if (fused) {
-        const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, hfull};
+        const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, hfull, pre};
         h->sample_fused(st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
         return;
     }
     hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, s, half, H, j0, hfull,
                        p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
     if (h->solver == 0 && h->sample) {
-        const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s, half, pd, j0, hfull};
+        const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s, half, pd, j0, hfull, nullptr};
         h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
     } else {
         h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
@@ -147,8 +148,11 @@ static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long
 // Kernels of n steps (both halves, all proposals) reading this chunk's RunArgs.
 static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
     for (int s = 0; s < n; ++s)
-        for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H);
+        for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H, p->d_pre);
 }
+
+// The fused half-step takes its draws from a per-chunk table when there is one.
+static bool uses_pre(const rvk_post *p) { return p->fusable && p->h->solver == 0 && p->h->sample_fused; }
 
 // The kStepsPerGraph-step chunk as a HIP graph, captured once per (H, solver) and
 // replayed: its kernel arguments never change (everything per call is in d_run).
@@ -186,6 +190,7 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_au);
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
+    (void)hipFree(p->d_pre);
     (void)hipFree(p->d_xin);
     (void)hipFree(p->d_oin);
     if (p->graph) (void)hipGraphExecDestroy(p->graph);
@@ -205,8 +210,10 @@ static int reserve_impl(rvk_post *p, long long W) {
     (void)hipFree(p->d_nlp);
     (void)hipFree(p->d_au);
     (void)hipFree(p->d_sidx);
+    (void)hipFree(p->d_pre);
     p->d_full = p->d_lp = p->d_q = p->d_fac = p->d_nlp = p->d_au = nullptr;
     p->d_sidx = nullptr;
+    p->d_pre = nullptr;
     p->capw = 0;
     const size_t w = (size_t)W;
     HIPCHK(hipMalloc(&p->d_full, sizeof(double) * w * (size_t)p->h->p_full()));
@@ -216,6 +223,7 @@ static int reserve_impl(rvk_post *p, long long W) {
     HIPCHK(hipMalloc(&p->d_nlp, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_au, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * w));
+    if (p->fusable) HIPCHK(hipMalloc(&p->d_pre, sizeof(PreDraw) * (size_t)kStepsPerGraph * 2 * w));
     p->capw = W;
     return RVK_OK;
 }
@@ -371,7 +379,13 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
                     seed,
                     step0 + (uint64_t)s0,
                     a};
-        hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+        if (uses_pre(p)) {
+            const long long np = (long long)n * 2 * H;
+            hipLaunchKernelGGL(set_run_draws_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, p->d_run,
+                               run, p->d_pre, n, H, p->n_free);
+        } else {
+            hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+        }
         if (use_graph && n == kStepsPerGraph) {
             if ((rc = ensure_graph(p, H))) return rc;
             HIPCHK(hipGraphLaunch(p->graph, st));
@@ -401,7 +415,7 @@ int rvk_stretch_half(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t 
     const RunArgs run{d_x, d_lp, (long long *)d_naccepted, (int *)d_status, nullptr, nullptr,
                       nullptr, nullptr, nullptr, nullptr, seed, step, a};
     hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
-    enqueue_half(p, st, 0, half, j0, count, H);
+    enqueue_half(p, st, 0, half, j0, count, H, nullptr);
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

@@ -165,6 +165,26 @@ __device__ __forceinline__ Draw draw(const RunArgs &r, int step, int half, long 
     return d;
 }
 
+// One proposal's draws as the fused half-step uses them, precomputed for a chunk of steps by
+// set_run_draws_kernel: the walker and its complement, z, (D - 1) log z and log u'.  The same
+// expressions as the fused kernel's in-kernel path (make_pre), so either gives the same bits.
+struct PreDraw {
+    double z, fac, lau;
+    long long s, c;
+};
+
+__device__ __forceinline__ PreDraw make_pre(const RunArgs &r, int step, int half, long long j, long long H, int D) {
+    const Draw dr = draw(r, step, half, j, H);
+    const double zt = (r.a - 1.0) * dr.zu + 1.0;
+    PreDraw p;
+    p.z = zt * zt / r.a;
+    p.fac = ((double)D - 1.0) * log(p.z);
+    p.lau = log(dr.au);
+    p.s = dr.s;
+    p.c = dr.c;
+    return p;
+}
+
 // Per-walker prologue, one wave per walker: x (n_free coordinates, in LDS `lx`)
 // -> full row (LDS `lf` and global `full`) and the log-prior, which is returned
 // in every lane.  Lanes work over columns, planets and prior slots; the slot
@@ -269,6 +289,7 @@ struct SampleArgs {
     PostDev pd;                 // the posterior (fused proposals, SAMPLE == 2)
     long long j0;               // the launch's proposals are j0 .. j0 + count - 1 of the half
     long long hfull;            // walkers per half (the complement's range; chain row stride / 2)
+    const PreDraw *pre;         // [steps][2][hfull] this chunk's draws, or nullptr (drawn in the kernel)
 };
 
 // Limits of the fused proposal path (loglike_kernel SAMPLE == 2): the proposal, its full row
@@ -304,6 +325,18 @@ static __global__ __launch_bounds__(256) void stretch_accept_kernel(const RunArg
 }
 
 static __global__ void set_run_kernel(RunArgs *dst, RunArgs v) { *dst = v; }
+
+// The chunk's arguments plus, for the fused half-step, every proposal's draws of its n steps
+// (one thread per proposal): the fused kernel then reads one PreDraw (a wave-uniform address)
+// instead of running two Philox blocks on its critical path.
+static __global__ __launch_bounds__(256) void set_run_draws_kernel(RunArgs *dst, RunArgs v, PreDraw *pre, int n,
+                                                                   long long H, int D) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *dst = v;
+    if (i >= (long long)n * 2 * H) return;
+    const long long sh = i / H;
+    pre[i] = make_pre(v, (int)(sh >> 1), (int)(sh & 1), i - sh * H, H, D);
+}
 
 
 }  // namespace rvk
