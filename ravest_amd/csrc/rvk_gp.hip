@@ -59,6 +59,12 @@ namespace {
 #ifndef RVK_GP_TRACE
 #define RVK_GP_TRACE 0    // timing experiments only: s_memtime per phase for the first walker of block 0
 #endif
+#ifndef RVK_GP_TWOCOL
+#define RVK_GP_TWOCOL 0   // each workspace tile read in P(k) serves columns k+1 and k+2 (see P(k))
+#endif
+#ifndef RVK_GP_BAL
+#define RVK_GP_BAL 1      // P(k)/S2(k) rows go to the waves that do not factor in step k (see prow)
+#endif
 #if RVK_GP_TRACE
 __device__ unsigned long long g_gp_trace[8][32][8];
 #define GP_HWID() (__builtin_amdgcn_s_getreg((31 << 11) | 4))   // HW_REG_HW_ID: wave, SIMD, CU ids
@@ -248,10 +254,30 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 }
             }
         };
+        // Tile row held in accumulator slot q during P(k) and S2(k).  The factor of step k is the
+        // step's serial critical path, so (RVK_GP_BAL) its wave f = k % NW takes no rows while the
+        // other NW - 1 waves can hold them: rows k+1, k+2, ... go round-robin over waves f+1, f+2,
+        // ..., so row k+1 (whose S2 result is the next diagonal tile, kept in registers as dacc)
+        // lands on wave (k+1) % NW, the factor wave of step k+1; rows past the others' MAXR slots
+        // (only in the first steps, where the row work is small) fall to wave f.  The accumulators
+        // are re-formed every step and parked in LDS between S2(k) and S1(k+1), so the assignment
+        // may change from step to step.  Otherwise: fixed round-robin ownership.
+        auto prow = [&](int k, int q) -> int {
+#if RVK_GP_BAL && !RVK_GP_TWOCOL
+            const int t = (wr - k % NW + NW) % NW;
+            return t ? k + t + (NW - 1) * q : k + 1 + (NW - 1) * MAXR + q;
+#else
+            (void)k;
+            return wr + NW * q;
+#endif
+        };
         double quad = 0.0;          // sum of y^2 over this wave's lanes
         double dp = 1.0;            // product of this wave's pivots L_ii^2, renormalised (x 2^pexp)
         int pexp = 0;
         f32x16 nacc[MAXR], dacc;
+#if RVK_GP_TWOCOL
+        f32x16 nacc2[MAXR];      // column k+2's partial sum, carried into step k+1 as nacc
+#endif
         // acc(bi, 0) = C(bi, 0): the diagonal tile in wave 0's registers, the rest parked
 #pragma unroll
         for (int q = 0; q < MAXR; ++q) {
@@ -266,6 +292,9 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                     for (int r = 0; r < 16; ++r) L.pan[(bi - 1) * TILE + r * 64 + lane] = t[r];
                 }
             }
+#if RVK_GP_TWOCOL
+            if (bi >= 1 && bi < nt) cov_tile(bi, 1, nacc2[q]);   // column 1 has no j < 0 terms
+#endif
         }
         __syncthreads();
 #if RVK_GP_TRACE
@@ -275,7 +304,13 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             GP_MARK(k, 0);
             // ---- P(k): factor the diagonal tile (wave k % NW) --------------------------------
 #pragma unroll
-            for (int q = 0; q < MAXR; ++q) nacc[q] = f32x16{};   // (ends the previous step's live ranges)
+            for (int q = 0; q < MAXR; ++q) {
+#if RVK_GP_TWOCOL
+                nacc[q] = nacc2[q];                   // column k+1: C and the j in S(k-1) terms
+#else
+                nacc[q] = f32x16{};                   // (ends the previous step's live ranges)
+#endif
+            }
             if (wr == k % NW && !(RVK_GP_ABLATE & 2)) {
                 // the factor is the step's critical path: its VALU chain goes ahead of the
                 // co-resident waves' instructions (MI355X_MICROARCH.md, two waves per SIMD)
@@ -368,10 +403,99 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             }
             GP_MARK(k, 1);
             // ---- P(k): the next column's tiles, all but the j = k term ------------------------
+#if RVK_GP_TWOCOL
+            // Two columns per workspace read.  Column c's sum over j < c - 1 is split between
+            // steps c - 2 and c - 1 by the parity of j: step k reads only the tiles of
+            // S(k) = {j < k : j = k + 1 (mod 2)} and applies each to column k+1 (completing it:
+            // S(k-1) and S(k) partition [0, k)) and to column k+2 (which step k+1 completes
+            // with S(k+1), the rest of [0, k+1)).  Every B tile is read once for two columns
+            // (half the left-looking re-reads) and each step does the same MFMA work as a
+            // one-column step.  The A tiles L(k+1, j), L(k+2, j) and the B tiles of two owned
+            // rows are streamed in half tiles (8 k-steps), double buffered.
             if (k + 1 < nt) {
+                const bool two = k + 2 < nt;
 #pragma unroll
                 for (int q = 0; q < MAXR; ++q) {
                     const int bi = wr + NW * q;
+                    if (two && bi >= k + 2 && bi < nt) cov_tile(bi, k + 2, nacc2[q]);
+                }
+                const long long lane_off = c * TB + 16 * h;
+                const int j0 = (k + 1) & 1;
+                auto pass = [&](auto q0c) {
+                    constexpr int Q0 = decltype(q0c)::value;
+                    constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
+                    bool any = false;
+#pragma unroll
+                    for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NW * q >= k + 1) && (wr + NW * q < nt);
+                    if (!any || k == 0) return;
+                    struct Ops {
+                        float4 a1[2], a2[2], b[R][2];
+                    };
+                    // half hf of the tiles of j (the trip past the end re-reads j0's: L1 hits, so
+                    // every load is unconditional and vmcnt waits are exact)
+                    auto issue = [&](Ops &o, int j, int hf) {
+                        const int jj = j < k ? j : j0;
+                        const int s1 = L.slot[(k + 1) * nt + jj];
+                        const int s2 = two ? L.slot[(k + 2) * nt + jj] : s1;
+                        const float4 *pa1 = reinterpret_cast<const float4 *>(A + s1 * TILE + lane_off) + 2 * hf;
+                        const float4 *pa2 = reinterpret_cast<const float4 *>(A + s2 * TILE + lane_off) + 2 * hf;
+                        o.a1[0] = pa1[0];
+                        o.a1[1] = pa1[1];
+                        o.a2[0] = pa2[0];
+                        o.a2[1] = pa2[1];
+#pragma unroll
+                        for (int q = 0; q < R; ++q) {
+                            const int bi = wr + NW * (Q0 + q);
+                            const bool live = bi >= k + 1 && bi < nt;
+                            const float4 *pb = reinterpret_cast<const float4 *>(
+                                                   A + L.slot[(live ? bi : k + 1) * nt + jj] * TILE + lane_off) + 2 * hf;
+                            o.b[q][0] = pb[0];
+                            o.b[q][1] = pb[1];
+                        }
+                    };
+                    auto consume = [&](const Ops &o) {
+#pragma unroll
+                        for (int q = 0; q < R; ++q) {
+                            const int bi = wr + NW * (Q0 + q);
+                            if (bi >= k + 1 && bi < nt) {
+                                f32x16 &acc = nacc[Q0 + q];
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) {
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a1[u].x, o.b[q][u].x, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a1[u].y, o.b[q][u].y, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a1[u].z, o.b[q][u].z, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a1[u].w, o.b[q][u].w, acc, 0, 0, 0);
+                                }
+                            }
+                            if (two && bi >= k + 2 && bi < nt) {
+                                f32x16 &acc = nacc2[Q0 + q];
+#pragma unroll
+                                for (int u = 0; u < 2; ++u) {
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a2[u].x, o.b[q][u].x, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a2[u].y, o.b[q][u].y, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a2[u].z, o.b[q][u].z, acc, 0, 0, 0);
+                                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a2[u].w, o.b[q][u].w, acc, 0, 0, 0);
+                                }
+                            }
+                        }
+                    };
+                    Ops X, Y;
+                    issue(X, j0, 0);
+                    for (int j = j0; j < k; j += 2) {
+                        issue(Y, j, 1);
+                        consume(X);
+                        issue(X, j + 2, 0);
+                        consume(Y);
+                    }
+                };
+                pass(std::integral_constant<int, 0>{});
+                if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
+            }
+#else
+            if (k + 1 < nt) {
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q) {
+                    const int bi = prow(k, q);
                     if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
                 }
                 // Operand tiles: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows
@@ -387,7 +511,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                     constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
                     bool any = false;
 #pragma unroll
-                    for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NW * q >= k + 1) && (wr + NW * q < nt);
+                    for (int q = Q0; q < Q0 + R; ++q) any |= prow(k, q) >= k + 1 && prow(k, q) < nt;
                     if (!any || k == 0) return;
                     struct Ops {
                         float4 a[4], b[R][4];
@@ -399,7 +523,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                         for (int u = 0; u < 4; ++u) o.a[u] = pa[u];
 #pragma unroll
                         for (int q = 0; q < R; ++q) {
-                            const int bi = wr + NW * (Q0 + q);
+                            const int bi = prow(k, Q0 + q);
                             const bool live = bi >= k + 1 && bi < nt;
                             const float4 *pb = reinterpret_cast<const float4 *>(
                                 A + L.slot[(live ? bi : k + 1) * nt + jj] * TILE + lane_off);
@@ -410,7 +534,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                     auto consume = [&](const Ops &o) {
 #pragma unroll
                         for (int q = 0; q < R; ++q) {
-                            const int bi = wr + NW * (Q0 + q);
+                            const int bi = prow(k, Q0 + q);
                             if (bi >= k + 1 && bi < nt) {
                                 f32x16 &acc = nacc[Q0 + q];
 #pragma unroll
@@ -435,6 +559,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 pass(std::integral_constant<int, 0>{});
                 if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
             }
+#endif
             GP_MARK(k, 2);
             __syncthreads();                                // B1: L_kk^-1 and y_k published
             GP_MARK(k, 3);
@@ -486,7 +611,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             for (int ks = 0; ks < 16; ++ks) lk[ks] = L.pan[k * TILE + ks * 64 + lane];
 #pragma unroll
             for (int q = 0; q < MAXR; ++q) {
-                const int bi = wr + NW * q;
+                const int bi = prow(k, q);
                 if (bi > k && bi < nt) {
                     const float *src = L.pan + (bi - 1) * TILE;
                     float sb[16];
