@@ -62,8 +62,20 @@ namespace {
 #ifndef RVK_GP_TWOCOL
 #define RVK_GP_TWOCOL 0   // each workspace tile read in P(k) serves columns k+1 and k+2 (see P(k))
 #endif
+#ifndef RVK_GP_HALF
+#define RVK_GP_HALF 1     // one-column P(k): operand tiles streamed in halves (no spills: 3.43 -> 3.21 ms)
+#endif
+#ifndef RVK_GP_QU
+#define RVK_GP_QU (RVK_GP_HALF ? 2 : 4)   // float4 per operand tile and register set (4 = whole tiles)
+#endif
+#ifndef RVK_GP_NBUF
+#define RVK_GP_NBUF 2     // operand register sets in the ring (NBUF - 1 in flight)
+#endif
 #ifndef RVK_GP_BAL
 #define RVK_GP_BAL 1      // P(k)/S2(k) rows go to the waves that do not factor in step k (see prow)
+#endif
+#ifndef RVK_GP_FU
+#define RVK_GP_FU 6       // RVK_GP_BAL == 2: the factor's cost in (row, j) accumulation units
 #endif
 #if RVK_GP_TRACE
 __device__ unsigned long long g_gp_trace[8][32][8];
@@ -263,7 +275,24 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
         // are re-formed every step and parked in LDS between S2(k) and S1(k+1), so the assignment
         // may change from step to step.  Otherwise: fixed round-robin ownership.
         auto prow = [&](int k, int q) -> int {
-#if RVK_GP_BAL && !RVK_GP_TWOCOL
+#if RVK_GP_BAL == 2 && !RVK_GP_TWOCOL
+            // the factor wave also takes the last rf rows when that shortens the step: in units
+            // of one (row, j) accumulation, the factor costs about RVK_GP_FU and a row k
+            const int m = nt - 1 - k;
+            int rf = m - (NW - 1) * MAXR > 0 ? m - (NW - 1) * MAXR : 0, best = 1 << 30;
+            for (int r = rf; r < MAXR && r <= m; ++r) {
+                const int tf = RVK_GP_FU + r * k, to = (m - r + NW - 2) / (NW - 1) * k;
+                const int tm = tf > to ? tf : to;
+                if (tm < best) {
+                    best = tm;
+                    rf = r;
+                }
+            }
+            const int no = m - rf, t = (wr - k % NW + NW) % NW;
+            if (!t) return k + 1 + no + q;
+            const int i = t - 1 + (NW - 1) * q;
+            return i < no ? k + 1 + i : nt;
+#elif RVK_GP_BAL && !RVK_GP_TWOCOL
             const int t = (wr - k % NW + NW) % NW;
             return t ? k + t + (NW - 1) * q : k + 1 + (NW - 1) * MAXR + q;
 #else
@@ -513,22 +542,27 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
 #pragma unroll
                     for (int q = Q0; q < Q0 + R; ++q) any |= prow(k, q) >= k + 1 && prow(k, q) < nt;
                     if (!any || k == 0) return;
+                    // QU float4 (2 QU k-steps of the 32x32x2 MFMA) per operand tile and register set:
+                    // whole tiles, or half tiles (RVK_GP_HALF: half the operand registers)
+                    constexpr int QU = RVK_GP_QU, NSET = 4 / QU, NB = RVK_GP_NBUF;
                     struct Ops {
-                        float4 a[4], b[R][4];
+                        float4 a[QU], b[R][QU];
                     };
-                    auto issue = [&](Ops &o, int j) {
-                        const int jj = j < k ? j : k - 1;
-                        const float4 *pa = reinterpret_cast<const float4 *>(A + L.slot[(k + 1) * nt + jj] * TILE + lane_off);
+                    const int T = NSET * k;
+                    auto issue = [&](Ops &o, int hx) {
+                        const int hh = hx < T ? hx : T - 1;
+                        const int jj = hh / NSET, part = hh % NSET;
+                        const float4 *pa = reinterpret_cast<const float4 *>(A + L.slot[(k + 1) * nt + jj] * TILE + lane_off) + QU * part;
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) o.a[u] = pa[u];
+                        for (int u = 0; u < QU; ++u) o.a[u] = pa[u];
 #pragma unroll
                         for (int q = 0; q < R; ++q) {
                             const int bi = prow(k, Q0 + q);
                             const bool live = bi >= k + 1 && bi < nt;
                             const float4 *pb = reinterpret_cast<const float4 *>(
-                                A + L.slot[(live ? bi : k + 1) * nt + jj] * TILE + lane_off);
+                                A + L.slot[(live ? bi : k + 1) * nt + jj] * TILE + lane_off) + QU * part;
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) o.b[q][u] = pb[u];
+                            for (int u = 0; u < QU; ++u) o.b[q][u] = pb[u];
                         }
                     };
                     auto consume = [&](const Ops &o) {
@@ -538,7 +572,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                             if (bi >= k + 1 && bi < nt) {
                                 f32x16 &acc = nacc[Q0 + q];
 #pragma unroll
-                                for (int u = 0; u < 4; ++u) {
+                                for (int u = 0; u < QU; ++u) {
                                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].x, o.b[q][u].x, acc, 0, 0, 0);
                                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].y, o.b[q][u].y, acc, 0, 0, 0);
                                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(o.a[u].z, o.b[q][u].z, acc, 0, 0, 0);
@@ -547,13 +581,17 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                             }
                         }
                     };
-                    Ops X, Y;
-                    issue(X, 0);
-                    for (int j = 0; j < k; j += 2) {
-                        issue(Y, j + 1);
-                        consume(X);
-                        issue(X, j + 2);
-                        if (j + 1 < k) consume(Y);
+                    // a ring of NB register sets: each trip issues one set and consumes one, so
+                    // NB - 1 sets are always in flight (trips past the end re-read the last set)
+                    Ops ring[NB];
+#pragma unroll
+                    for (int b = 0; b + 1 < NB; ++b) issue(ring[b], b);
+                    for (int hx = 0; hx < T; hx += NB) {
+#pragma unroll
+                        for (int b = 0; b < NB; ++b) {
+                            issue(ring[(b + NB - 1) % NB], hx + b + NB - 1);
+                            if (b == 0 || hx + b < T) consume(ring[b]);
+                        }
                     }
                 };
                 pass(std::integral_constant<int, 0>{});
