@@ -74,6 +74,9 @@ namespace {
 #ifndef RVK_GP_BAL
 #define RVK_GP_BAL 1      // P(k)/S2(k) rows go to the waves that do not factor in step k (see prow)
 #endif
+#ifndef RVK_GP_SPLIT
+#define RVK_GP_SPLIT 0    // mid steps: (row, j) units split evenly over the row waves (see plan; measured = base)
+#endif
 #ifndef RVK_GP_FU
 #define RVK_GP_FU 6       // RVK_GP_BAL == 2: the factor's cost in (row, j) accumulation units
 #endif
@@ -300,6 +303,65 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             return wr + NW * q;
 #endif
         };
+        // The step's accumulation plan: slot q holds row bi[q] over j in [lo[q], hi[q]).  Whole
+        // rows (prow) in the first and last steps; in the middle steps (RVK_GP_SPLIT) the m k
+        // (row, j) units are split evenly over the NW - 1 row waves in row-major order, so
+        // the waves' shares differ by at most one unit instead of one row.  A row cut at a
+        // wave boundary is started (C and its first j's) by the lower wave, which finishes it
+        // in S2; the upper wave accumulates its tail from zero and parks that partial in a
+        // free panel slot (rows <= k-1 are finished), alternating between two slot sets by
+        // the parity of k so the next step's parking never meets this step's S2 read.
+        struct Plan {
+            int bi[MAXR], lo[MAXR], hi[MAXR];
+            int sec_slot;     // >= 0: slot 0 is a row tail; park its partial at pan[sec_slot]
+            int add_q;        // >= 0: the next wave parks the tail of row bi[add_q] at pan[add_slot]
+            int add_slot;
+        };
+        auto plan = [&](int k) -> Plan {
+            Plan P;
+            P.sec_slot = -1;
+            P.add_q = -1;
+            P.add_slot = 0;
+#pragma unroll
+            for (int q = 0; q < MAXR; ++q) {
+                P.bi[q] = prow(k, q);
+                P.lo[q] = 0;
+                P.hi[q] = k;
+            }
+#if RVK_GP_SPLIT && RVK_GP_BAL == 1 && !RVK_GP_TWOCOL
+            constexpr int NA = NW - 1;
+            const int m = nt - 1 - k, ut = m * k;
+            bool split = NA > 1 && k >= 2 * NA - 1 && m >= NA && m <= NA * MAXR;
+            for (int t = 1; t <= NA && split; ++t) {      // every wave's rows must fit its slots
+                const int s0 = (t - 1) * ut / NA, e0 = t * ut / NA;
+                split = e0 > s0 && (e0 - 1) / k - s0 / k < MAXR;
+            }
+            if (split) {
+                const int t = (wr - k % NW + NW) % NW;
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q) P.bi[q] = nt;
+                if (t) {
+                    const int s0 = (t - 1) * ut / NA, e0 = t * ut / NA;
+                    const int rs = s0 / k, re = (e0 - 1) / k;
+#pragma unroll
+                    for (int q = 0; q < MAXR; ++q) {
+                        const int ri = rs + q;
+                        if (ri <= re) {
+                            P.bi[q] = k + 1 + ri;
+                            P.lo[q] = ri == rs ? s0 - rs * k : 0;
+                            P.hi[q] = ri == re ? e0 - re * k : k;
+                        }
+                    }
+                    if (s0 > rs * k) P.sec_slot = (t - 2) + (NA - 1) * (k & 1);
+                    if (e0 - re * k < k) {
+                        P.add_q = re - rs;
+                        P.add_slot = (t - 1) + (NA - 1) * (k & 1);
+                    }
+                }
+            }
+#endif
+            return P;
+        };
         double quad = 0.0;          // sum of y^2 over this wave's lanes
         double dp = 1.0;            // product of this wave's pivots L_ii^2, renormalised (x 2^pexp)
         int pexp = 0;
@@ -521,55 +583,65 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
             }
 #else
+            const Plan P = plan(k);
             if (k + 1 < nt) {
 #pragma unroll
                 for (int q = 0; q < MAXR; ++q) {
-                    const int bi = prow(k, q);
-                    if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
+                    const int bi = P.bi[q];
+                    if (bi >= k + 1 && bi < nt) {
+                        if (P.lo[q] == 0) cov_tile(bi, k + 1, nacc[q]);
+                        else nacc[q] = f32x16{};              // a row's tail: its partial sum only
+                    }
                 }
-                // Operand tiles: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows
-                // at a time (rows q0, q0 + 1; a second pass takes rows 2, 3 and re-reads the A
-                // tiles from L2).  Two register sets X / Y alternate over j (the loop is unrolled
-                // by two), so the next j's tiles are in flight during this j's MFMAs.  Finished
-                // rows (and the trip past the end) re-read the A tile, an L1 hit, so every load
-                // is unconditional and every path through the loop leaves the same loads
-                // outstanding (exact s_waitcnt vmcnt).
+                // Operand tiles: the A tile L(k+1, j) and the B tiles L(bi, j) of two of the
+                // step's rows at a time (slots q0, q0 + 1; a second pass takes slots 2, 3 and
+                // re-reads the A tiles from L2), streamed in QU-float4 sets through a ring of NB
+                // register sets, so NB - 1 sets are in flight during a set's MFMAs.  The pass runs
+                // over the union of its rows' j ranges; a row outside its range (or finished, or
+                // the trip past the end) re-reads the A tile, an L1 hit, so every load is
+                // unconditional and every path leaves the same loads outstanding (exact vmcnt).
                 const long long lane_off = c * TB + 16 * h;
                 auto pass = [&](auto q0c) {
                     constexpr int Q0 = decltype(q0c)::value;
                     constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
-                    bool any = false;
-#pragma unroll
-                    for (int q = Q0; q < Q0 + R; ++q) any |= prow(k, q) >= k + 1 && prow(k, q) < nt;
-                    if (!any || k == 0) return;
-                    // QU float4 (2 QU k-steps of the 32x32x2 MFMA) per operand tile and register set:
-                    // whole tiles, or half tiles (RVK_GP_HALF: half the operand registers)
                     constexpr int QU = RVK_GP_QU, NSET = 4 / QU, NB = RVK_GP_NBUF;
+                    bool any = false;
+                    int jmin = k, jmax = 0;
+#pragma unroll
+                    for (int q = Q0; q < Q0 + R; ++q) {
+                        if (P.bi[q] >= k + 1 && P.bi[q] < nt) {
+                            any = true;
+                            jmin = P.lo[q] < jmin ? P.lo[q] : jmin;
+                            jmax = P.hi[q] > jmax ? P.hi[q] : jmax;
+                        }
+                    }
+                    if (!any || k == 0) return;
                     struct Ops {
                         float4 a[QU], b[R][QU];
                     };
-                    const int T = NSET * k;
+                    const int H0 = NSET * jmin, H1 = NSET * jmax;
+                    auto in_range = [&](int q, int jj) {
+                        return P.bi[Q0 + q] >= k + 1 && P.bi[Q0 + q] < nt && jj >= P.lo[Q0 + q] && jj < P.hi[Q0 + q];
+                    };
                     auto issue = [&](Ops &o, int hx) {
-                        const int hh = hx < T ? hx : T - 1;
+                        const int hh = hx < H1 ? hx : H1 - 1;
                         const int jj = hh / NSET, part = hh % NSET;
                         const float4 *pa = reinterpret_cast<const float4 *>(A + L.slot[(k + 1) * nt + jj] * TILE + lane_off) + QU * part;
 #pragma unroll
                         for (int u = 0; u < QU; ++u) o.a[u] = pa[u];
 #pragma unroll
                         for (int q = 0; q < R; ++q) {
-                            const int bi = prow(k, Q0 + q);
-                            const bool live = bi >= k + 1 && bi < nt;
                             const float4 *pb = reinterpret_cast<const float4 *>(
-                                A + L.slot[(live ? bi : k + 1) * nt + jj] * TILE + lane_off) + QU * part;
+                                A + L.slot[(in_range(q, jj) ? P.bi[Q0 + q] : k + 1) * nt + jj] * TILE + lane_off) + QU * part;
 #pragma unroll
                             for (int u = 0; u < QU; ++u) o.b[q][u] = pb[u];
                         }
                     };
-                    auto consume = [&](const Ops &o) {
+                    auto consume = [&](const Ops &o, int hx) {
+                        const int jj = hx / NSET;
 #pragma unroll
                         for (int q = 0; q < R; ++q) {
-                            const int bi = prow(k, Q0 + q);
-                            if (bi >= k + 1 && bi < nt) {
+                            if (in_range(q, jj)) {
                                 f32x16 &acc = nacc[Q0 + q];
 #pragma unroll
                                 for (int u = 0; u < QU; ++u) {
@@ -581,21 +653,23 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                             }
                         }
                     };
-                    // a ring of NB register sets: each trip issues one set and consumes one, so
-                    // NB - 1 sets are always in flight (trips past the end re-read the last set)
                     Ops ring[NB];
 #pragma unroll
-                    for (int b = 0; b + 1 < NB; ++b) issue(ring[b], b);
-                    for (int hx = 0; hx < T; hx += NB) {
+                    for (int b = 0; b + 1 < NB; ++b) issue(ring[b], H0 + b);
+                    for (int hx = H0; hx < H1; hx += NB) {
 #pragma unroll
                         for (int b = 0; b < NB; ++b) {
                             issue(ring[(b + NB - 1) % NB], hx + b + NB - 1);
-                            if (b == 0 || hx + b < T) consume(ring[b]);
+                            if (b == 0 || hx + b < H1) consume(ring[b], hx + b);
                         }
                     }
                 };
                 pass(std::integral_constant<int, 0>{});
                 if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
+                if (P.sec_slot >= 0) {                      // a row's tail: park the partial sum
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) L.pan[P.sec_slot * TILE + r * 64 + lane] = nacc[0][r];
+                }
             }
 #endif
             GP_MARK(k, 2);
@@ -649,8 +723,17 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
             for (int ks = 0; ks < 16; ++ks) lk[ks] = L.pan[k * TILE + ks * 64 + lane];
 #pragma unroll
             for (int q = 0; q < MAXR; ++q) {
+#if RVK_GP_TWOCOL
                 const int bi = prow(k, q);
                 if (bi > k && bi < nt) {
+#else
+                const int bi = P.bi[q];
+                if (bi > k && bi < nt && !(q == 0 && P.sec_slot >= 0)) {   // (a tail: the lower wave's row)
+                    if (q == P.add_q) {                     // the upper wave's partial of this row
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) nacc[q][r] += L.pan[P.add_slot * TILE + r * 64 + lane];
+                    }
+#endif
                     const float *src = L.pan + (bi - 1) * TILE;
                     float sb[16];
 #pragma unroll

@@ -3,6 +3,8 @@
 O=gpurun_out/${1:-gptc}
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_gp.py tests/test_gpu_gp64.py -x -q --timeout 120 --timeout-method thread > $O/pytest_base.log 2>&1 || { tail -40 $O/pytest_base.log; exit 1; }
+echo "base: $(tail -1 $O/pytest_base.log)"
 for so in build/variants/librvk_*.so; do
   v=$(basename $so .so)
   RAVEST_AMD_LIB=$so timeout -k 10 200 python -u -m pytest tests/test_gpu_gp.py -x -q --timeout 120 --timeout-method thread > $O/pytest_$v.log 2>&1 || { tail -40 $O/pytest_$v.log; exit 1; }
