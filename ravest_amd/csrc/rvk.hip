@@ -55,6 +55,9 @@ namespace {
                                       // (NP = 1 in VGPRs: 34 -> 7 SGPR spills, -2.5 % config 2;
                                       //  NP = 3 in VGPRs: +3.6 %)
 #endif
+#ifndef RVK_SAMPLE_BLOCK
+#define RVK_SAMPLE_BLOCK 512          // threads per fused half-step block: one block per CU at H = 2048 (256: 18.8, 512: 18.2, 768: 20.9 us per step)
+#endif
 #ifndef RVK_LL_BLOCK
 #define RVK_LL_BLOCK 1024             // threads per loglike_kernel block for NP = 1 and W >= 256 blocks' worth
                                       // (one wave preps 16 walkers: -7 % "P K e w Tc", +-0 "P K e w Tp")
@@ -733,9 +736,9 @@ void launch_sample_fused(hipStream_t st, EpochData d, int n, int ni, const doubl
                          PostArgs post, const SampleArgs &sa) {
     long long blocks;
     int wb;
-    ll_grid<NP>(H, blocks, wb);
-    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, 2>), dim3((unsigned)blocks), dim3(kBlock), 0, st, d, n,
-                       ni, rows, H, stride, wb, nullptr, post, sa);
+    ll_grid<NP>(H, blocks, wb, RVK_SAMPLE_BLOCK / 64);
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, 2, RVK_SAMPLE_BLOCK>), dim3((unsigned)blocks),
+                       dim3(RVK_SAMPLE_BLOCK), 0, st, d, n, ni, rows, H, stride, wb, nullptr, post, sa);
 }
 
 template <bool MULTI, int SOLVER, bool TP>
