@@ -68,6 +68,9 @@ namespace {
 #ifndef RVK_GP_QU
 #define RVK_GP_QU (RVK_GP_HALF ? 2 : 4)   // float4 per operand tile and register set (4 = whole tiles)
 #endif
+#ifndef RVK_GP_RPASS
+#define RVK_GP_RPASS 2    // rows per accumulation pass (the A tiles are re-read once per pass)
+#endif
 #ifndef RVK_GP_NBUF
 #define RVK_GP_NBUF 2     // operand register sets in the ring (NBUF - 1 in flight)
 #endif
@@ -603,7 +606,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 const long long lane_off = c * TB + 16 * h;
                 auto pass = [&](auto q0c) {
                     constexpr int Q0 = decltype(q0c)::value;
-                    constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
+                    constexpr int R = (MAXR - Q0) < RVK_GP_RPASS ? (MAXR - Q0) : RVK_GP_RPASS;
                     constexpr int QU = RVK_GP_QU, NSET = 4 / QU, NB = RVK_GP_NBUF;
                     bool any = false;
                     int jmin = k, jmax = 0;
@@ -665,7 +668,9 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                     }
                 };
                 pass(std::integral_constant<int, 0>{});
-                if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
+                if constexpr (MAXR > RVK_GP_RPASS) pass(std::integral_constant<int, RVK_GP_RPASS>{});
+                if constexpr (MAXR > 2 * RVK_GP_RPASS) pass(std::integral_constant<int, 2 * RVK_GP_RPASS>{});
+                if constexpr (MAXR > 3 * RVK_GP_RPASS) pass(std::integral_constant<int, 3 * RVK_GP_RPASS>{});
                 if (P.sec_slot >= 0) {                      // a row's tail: park the partial sum
 #pragma unroll
                     for (int r = 0; r < 16; ++r) L.pan[P.sec_slot * TILE + r * 64 + lane] = nacc[0][r];
