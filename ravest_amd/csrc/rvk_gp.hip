@@ -54,7 +54,7 @@ namespace {
 #define RVK_GP_AGPR 0     // accumulators in AGPRs (MFMA C/D off the VGPR file)
 #endif
 #ifndef RVK_GP_FACTOR_LDS
-#define RVK_GP_FACTOR_LDS 0   // diagonal factor: row broadcasts through LDS (1) or v_readlane (0); measured equal
+#define RVK_GP_FACTOR_LDS 1   // diagonal factor: row broadcasts through LDS (1) or v_readlane (0); with the balanced schedule 1 is 2 % faster
 #endif
 #ifndef RVK_GP_TRACE
 #define RVK_GP_TRACE 0    // timing experiments only: s_memtime per phase for the first walker of block 0
