@@ -165,14 +165,47 @@ def valu_roofline(pmc: dict | None, kern_ms: float) -> dict | None:
             "source": (pmc.get("source") or "") + " (profiles/%s)" % pmc.get("_file", "")}
 
 
+def csrc_digest() -> str:
+    """sha256 over the kernel sources and build flags (ravest_amd/csrc/*, include/*.h,
+    ravest_amd/Makefile), names and bytes, sorted: the provenance stamp of every
+    profiles/pmc_*.json (tools/pmc_summary.py writes it; the .git directory does not travel
+    to the GPU box, so the stamp is a content hash, not a commit id)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "ravest_amd", "csrc", "*")) +
+                   glob.glob(os.path.join(ROOT, "include", "*.h")) + [os.path.join(ROOT, "ravest_amd", "Makefile")])
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
+
+
 def load_pmc_file(name):
+    """A committed PMC summary, or None when it was measured on other kernel sources than this
+    tree's (its csrc_sha256 stamp differs from csrc_digest()): a stale counter file must not
+    turn a kernel change into a silently wrong fraction."""
     p = os.path.join(ROOT, "profiles", name)
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
         d["_file"] = name
+        if d.get("csrc_sha256") != csrc_digest():
+            return None
         return d
     return None
+
+
+def pmc_provenance(name) -> dict:
+    p = os.path.join(ROOT, "profiles", name)
+    stamp = None
+    if os.path.exists(p):
+        with open(p) as f:
+            stamp = json.load(f).get("csrc_sha256")
+    return {"file": "profiles/" + name, "csrc_sha256": stamp, "tree_csrc_sha256": csrc_digest(),
+            "matches_tree": stamp is not None and stamp == csrc_digest()}
 
 
 def graph_kernel_ms(launch, G: int = 20, reps: int = 10) -> float:
@@ -227,8 +260,9 @@ def config_line(cfg: int, W: int | None = None, label: str | None = None) -> dic
             "kernel_ms": ms, "kepler_solves_per_s": W * n_ep * n_pl / (ms * 1e-3),
             "walker_evals_per_s": W / (ms * 1e-3),
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS, "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                         "valu": valu_roofline(pmc, ms)},
+                         "frac": gbs / HBM_PEAK_GBS, "traffic": (pmc or {}).get("fabric_bytes_per_launch"),
+                         "valu": valu_roofline(pmc, ms),
+                         "pmc": pmc_provenance(f"pmc_{label or 'config%d' % cfg}.json")},
             "n_masked_walkers": int((~np.isfinite(ll)).sum()),
             "logprob_agreement": agreement(ds, ds.theta, ll, 1)}
 
@@ -342,7 +376,8 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     from ravest_amd.synth import make_gp_config
     ds, th, hy = make_gp_config(W, n_epochs=n)
     gp = GPLogLikelihood(ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments, ds.planet_letters,
-                         ds.parameterisation, GPKernel("Quasiperiodic"), device=torch.cuda.current_device())
+                         ds.parameterisation, GPKernel("Quasiperiodic"), device=torch.cuda.current_device(),
+                         precision="fp32+fp64")
     dev = torch.device("cuda", torch.cuda.current_device())
     tt, ht = torch.from_numpy(th).to(dev), torch.from_numpy(hy).to(dev)
     out = torch.empty(W, dtype=torch.float64, device=dev)
@@ -385,10 +420,14 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     return {"config": f"config 5: 1 planet + quasi-periodic GP, {n} epochs, {W} walkers, fp32 factorisation",
             "ms_per_eval": ms, "walker_evals_per_s": W / (ms * 1e-3),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                         "frac": tf / FP32_MFMA_PEAK_TF, "traffic": (load_pmc_file("pmc_config5.json") or {}).get("hbm_bytes_per_launch"),
+                         "frac": tf / FP32_MFMA_PEAK_TF,
+                         "traffic": (load_pmc_file("pmc_config5.json") or {}).get("fabric_bytes_per_launch"),
+                         "pmc": pmc_provenance("pmc_config5.json"),
                          "note": "algorithmic FLOP = W*(n^3/3 + 2n^2) per launch / launch duration; traffic = "
-                                 "L2 memory-side bytes per launch (PMC, profiles/pmc_config5.json; includes "
-                                 "Infinity-Cache hits: the workspace tiles re-read by the left-looking update)"},
+                                 "L2 memory-side (fabric) bytes per launch, FETCH_SIZE x 2 + WRITE_SIZE as "
+                                 "MI355X_MICROARCH.md prescribes (PMC, profiles/pmc_config5.json): it counts "
+                                 "Infinity-Cache hits too -- the workspace tiles re-read by the left-looking "
+                                 "update -- so it bounds HBM bytes from above"},
             "n_masked_walkers": int((~np.isfinite(out.cpu().numpy())).sum()),
             "precision": "fp32 factorisation, fp64 re-evaluation of walkers it rejects (default)",
             "max_rel_err_vs_fp64_oracle": rel(o32),
@@ -430,11 +469,16 @@ def predictive_line(eng, theta, S: int = 100_000, T: int = 1000, reps: int = 5) 
     gbs = nbytes / (ms * 1e-3) / 1e9
     ok = bool(torch.isfinite(out).all().item())
     del out
+    pmc = load_pmc_file("pmc_predictive.json")
     return {"what": f"posterior predictive, {S} samples x {T} times, 1 planet + trend, fp64 [S, T] output in HBM",
             "ms_per_call": ms, "kepler_solves_per_s": S * T / (ms * 1e-3), "all_finite": ok,
-            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS,
-                         "note": "bytes = 8*S*T output + 8*S*P_full samples + 8*T times per launch / launch time"}}
+            "roofline": {"bound": "valu-fp64", "valu": valu_roofline(pmc, ms),
+                         "pmc": pmc_provenance("pmc_predictive.json"),
+                         "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                 "traffic": (pmc or {}).get("fabric_bytes_per_launch")},
+                         "note": "the Kepler solves bind it (fp64 VALU, 'valu': PMC counters of the same kernel, "
+                                 "null unless measured on this tree's sources); hbm = 8*S*T output + 8*S*P_full "
+                                 "samples + 8*T times per launch / launch time"}}
 
 
 def main():
@@ -586,7 +630,7 @@ def main():
         alg_bytes = W * (n_ep * BYTES_PER_WALKER_EPOCH + theta.shape[1] * 8 + 8)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         pmc = load_pmc_file(f"pmc_config{args.config}.json")
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        traffic = pmc.get("fabric_bytes_per_launch") if pmc else None
         valu = valu_roofline(pmc, kern_ms)
         line = {
             "metric": "walker-log-prob evals/sec (= Kepler solves/sec) at 1/2/4/8 MI355X",
@@ -594,7 +638,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"config {args.config}: {n_pl} planet(s), {n_ep} epochs, {W} walkers per GPU, "
-                                   f"fp64, theta resident in HBM" + (", RCCL all-gather of log-probs" if world > 1 else ""),
+                                   f"fp64, theta resident in HBM" + (
+                                       (", RCCL all-gather of log-probs" if backend == "nccl" else
+                                        f", {backend} all-gather of log-probs (host-staged rehearsal)")
+                                       if world > 1 else ""),
                        "n_planets": n_pl, "n_epochs": n_ep, "walkers_per_gpu": W, "n_inst": n_in,
                        "parameterisation": ds.parameterisation.parameterisation,
                        "parallelism": f"walker-shard x{world}"},
@@ -606,12 +653,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "achieved_per_step": alg_bytes / (el / args.steps) / 1e9,
-                         "valu": valu,
+                         "valu": valu, "pmc": pmc_provenance(f"pmc_config{args.config}.json"),
                          "note": "achieved = algorithmic bytes W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY "
                                  "§8(d)) / average kernel duration (HIP events around each G-launch graph replay "
-                                 "in the timed region / G); traffic = PMC HBM bytes per launch (the epoch arrays "
-                                 "are re-read from L2/MALL, not HBM). The binding resource is fp64 VALU issue: "
-                                 "'valu' (PMC counters of the same kernel)."},
+                                 "in the timed region / G); traffic = L2 memory-side (fabric) bytes per launch, "
+                                 "FETCH_SIZE x 2 + WRITE_SIZE (PMC; counts Infinity-Cache hits, so an upper bound "
+                                 "on HBM bytes: the epoch arrays are re-read from L2/MALL). The binding resource "
+                                 "is fp64 VALU issue: 'valu' (PMC counters of the same kernel, null unless "
+                                 "pmc.matches_tree: measured on this tree's kernel sources)."},
         }
         line["n_masked_walkers"] = int((~np.isfinite(ll)).sum())
         line["logprob_agreement"] = agreement(ds, theta, ll, world)

@@ -18,10 +18,10 @@
  *   RVK_GP_FP32                fp32 blocked Cholesky on MFMA (BASELINE config 5 is
  *                              fp32); a covariance that is not positive definite in
  *                              fp32 gives NaN;
- *   RVK_GP_FP32_FP64_FALLBACK  (default) as RVK_GP_FP32, then every walker the fp32
+ *   RVK_GP_FP32_FP64_FALLBACK  as RVK_GP_FP32, then every walker the fp32
  *                              factorisation rejected (NaN) is re-evaluated in fp64 in
  *                              the same stream-ordered call -- no host round trip;
- *   RVK_GP_FP64                fp64 throughout (the reference's precision: ravest runs
+ *   RVK_GP_FP64                (default) fp64 throughout (the reference's precision: ravest runs
  *                              tinygp with jax_enable_x64, fit.py:39); NaN only where
  *                              the covariance is not positive definite in fp64.
  * An invalid planet gives -inf (the reference's mean-model fail-fast).

@@ -939,7 +939,7 @@ unsigned gp_wave_blocks(long long n) {
 
 struct rvk_gp {
     rvk_handle *h = nullptr;
-    int mode = RVK_GP_FP32_FP64_FALLBACK;
+    int mode = RVK_GP_FP64;                  // the reference's precision (fit.py:39)
     gp_launch_t launch = nullptr;
     unsigned grid = 0;           // concurrent walkers (one workgroup each)
     size_t lds = 0;

@@ -11,10 +11,10 @@ with gamma = 1 / (2 lambda_p^2) (gp.py:126-156).
 ``GPLogLikelihood`` has the reference's constructor and ``__call__(params,
 hyperparams) -> float`` (fit.py:7942-8105), plus ``batch(theta_full, hyper)``
 over a walker block.  The factorisation precision is a constructor option
-(include/rvk_gp.h): "fp32+fp64" (default: fp32 MFMA Cholesky -- config 5 is
-fp32 -- with the walkers it rejects as not positive definite re-evaluated in
-fp64), "fp32", or "fp64" (the reference's own precision, jax_enable_x64,
-fit.py:39).  An invalid planet gives -inf like the reference's mean-model
+(include/rvk_gp.h): "fp64" (default: the reference's own precision,
+jax_enable_x64, fit.py:39), "fp32+fp64" (opt-in: fp32 MFMA Cholesky -- BASELINE
+config 5 is fp32 -- with the walkers it rejects as not positive definite
+re-evaluated in fp64) or "fp32".  An invalid planet gives -inf like the reference's mean-model
 fail-fast.
 
 ``GPLogPosterior`` mirrors fit.py:7596-7939 (jitter check, hyperparameter
@@ -105,7 +105,7 @@ class GPLogLikelihood:
 
     def __init__(self, time, vel, velerr, t0, instrument, unique_instruments, planet_letters,
                  parameterisation: Parameterisation, gp_kernel: GPKernel, device: int = -1,
-                 precision: str = "fp32+fp64") -> None:
+                 precision: str = "fp64") -> None:
         parameterisation = as_parameterisation(parameterisation)   # str, ours or ravest's own object
         if precision not in PRECISION:
             raise ValueError(f"precision must be one of {list(PRECISION)}, got {precision!r}")
@@ -198,7 +198,7 @@ class GPLogPosterior:
     def __init__(self, planet_letters, parameterisation, gp_kernel: GPKernel, priors: dict, hyperpriors: dict,
                  fixed_params: dict, fixed_hyperparams: dict, free_params_names: list, free_hyperparams_names: list,
                  time, vel, velerr, t0: float, instrument, unique_instruments, device: int = -1,
-                 precision: str = "fp32+fp64") -> None:
+                 precision: str = "fp64") -> None:
         from .posterior import LogPosterior, LogPrior
         self.planet_letters = planet_letters
         self.parameterisation = as_parameterisation(parameterisation)   # ravest's own object accepted

@@ -1,8 +1,10 @@
-"""Batched quasi-periodic GP log-likelihood (rvk_gp, fp32 factorisation) against the fp64
-restatement of tinygp's DirectSolver path (oracle/gp_oracle.py; parity unpinned at the tinygp
-boundary, see that module's header).
+"""Batched quasi-periodic GP log-likelihood (rvk_gp, the opt-in "fp32+fp64" precision: fp32 MFMA
+factorisation, BASELINE config 5) against the fp64 restatement of tinygp's DirectSolver path
+(oracle/gp_oracle.py; parity unpinned at the tinygp boundary, see that module's header).  The
+drop-in's default precision is fp64 (the reference's, fit.py:39), tested in test_gpu_gp64.py.
 
-Tolerance (stated): |ll - ll64| <= 2e-4 |ll64| + 0.05 per walker -- the fp32 Cholesky's
+Tolerance (stated): |ll - ll64| <= 3e-5 |ll64| + 1e-3 per walker, about 10x the worst error
+measured on these cases (config 5 on the driver's box: 2.4e-6 relative) -- the fp32 Cholesky's
 backward error grows with N and the covariance's condition number; identical -inf mask
 (invalid planets)."""
 import numpy as np
@@ -10,7 +12,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-RTOL, ATOL = 2e-4, 0.05
+RTOL, ATOL = 3e-5, 1e-3
 
 
 def _check(ll, ref, what):
@@ -26,7 +28,7 @@ def _check(ll, ref, what):
 def _gp(ds, n_inst=1):
     from ravest_amd.gp import GPKernel, GPLogLikelihood
     return GPLogLikelihood(ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments,
-                           ds.planet_letters, ds.parameterisation, GPKernel("Quasiperiodic"))
+                           ds.planet_letters, ds.parameterisation, GPKernel("Quasiperiodic"), precision="fp32+fp64")
 
 
 @pytest.mark.parametrize("n,np_,ni,par,trend", [(512, 1, 1, "P K e w Tp", False), (100, 1, 2, "P K e w Tc", True),
@@ -92,7 +94,8 @@ def test_gp_config5_shape_and_paths():
 
 
 def test_gp_reference_fixture_values():
-    """The reference's own GP test data (tests/test_fit.py:1549-1575): finite, and the fp64 value."""
+    """The reference's own GP test data (tests/test_fit.py:1549-1575): finite, and the fp64 value
+    at the drop-in's default precision (fp64) to the fp64 bar."""
     from oracle import gp_oracle
     from ravest_amd.gp import GPKernel, GPLogLikelihood
     time = np.array([0.0, 1.0, 2.0, 3.0, 4.0, 5.0])
@@ -108,7 +111,8 @@ def test_gp_reference_fixture_values():
     row = np.array([[params[n] for n in ll.names]])
     ref = gp_oracle.gp_loglike(time, vel, velerr, np.zeros(6, np.int32), 1, 1, 1, 2.0, row,
                                np.array([[1.0, 50.0, 0.5, 10.0]]))[0]
-    assert abs(got - ref) <= 1e-5 * abs(ref) + 1e-4
+    assert ll.precision == "fp64"
+    assert abs(got - ref) <= 1e-9 * max(1.0, abs(ref))
     bad = dict(params, P_b=-1.0)                 # tests/test_fit.py:1577-1600: invalid planet -> -inf
     assert ll(bad, hyper) == -np.inf
 

@@ -14,7 +14,7 @@ def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     ds, th, hy = make_gp_config(W, n_epochs=512)
     gp = GPLogLikelihood(ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments, ds.planet_letters,
-                         ds.parameterisation, GPKernel("Quasiperiodic"), device=0)
+                         ds.parameterisation, GPKernel("Quasiperiodic"), device=0, precision="fp32+fp64")
     tt, ht = torch.from_numpy(th).cuda(), torch.from_numpy(hy).cuda()
     out = torch.empty(W, dtype=torch.float64, device="cuda")
     for _ in range(2):
