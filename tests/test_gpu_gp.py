@@ -3,24 +3,25 @@ factorisation, BASELINE config 5) against the fp64 restatement of tinygp's Direc
 (oracle/gp_oracle.py; parity unpinned at the tinygp boundary, see that module's header).  The
 drop-in's default precision is fp64 (the reference's, fit.py:39), tested in test_gpu_gp64.py.
 
-Tolerance (stated): |ll - ll64| <= 3e-5 |ll64| + 1e-3 per walker, about 10x the worst error
-measured on these cases (config 5 on the driver's box: 2.4e-6 relative) -- the fp32 Cholesky's
-backward error grows with N and the covariance's condition number; identical -inf mask
-(invalid planets)."""
+Tolerance (stated): |ll - ll64| <= 3e-8 n |ll64| + 1e-3 per walker (n epochs: the fp32 Cholesky's
+backward error grows with n and the covariance's condition number), 2-30x the worst error
+measured on each case (n = 1024: 1.3e-5 relative vs a 3.1e-5 bar; config 5, n = 512: 2.4e-6 vs
+1.5e-5); identical -inf mask (invalid planets)."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-RTOL, ATOL = 3e-5, 1e-3
+RTOL_PER_EPOCH, ATOL = 3e-8, 1e-3
 
 
-def _check(ll, ref, what):
+def _check(ll, ref, what, n):
     fin = np.isfinite(ref)
     assert np.array_equal(np.isfinite(ll), fin), f"{what}: mask differs"
     assert np.all(ll[~fin] == -np.inf)
     err = np.abs(ll[fin] - ref[fin])
-    tol = RTOL * np.abs(ref[fin]) + ATOL
+    tol = RTOL_PER_EPOCH * n * np.abs(ref[fin]) + ATOL
+    print(f"[{what}] max |d|/|ref| {np.max(err / np.abs(ref[fin])):.3e}, worst {np.max(err / tol):.3f} x tol")
     assert np.all(err <= tol), f"{what}: worst {np.max(err / tol):.2f} x tol, max abs err {err.max():.3g}"
     return float(np.max(err / np.abs(ref[fin])))
 
@@ -51,7 +52,7 @@ def test_gp_loglike_vs_fp64_oracle(n, np_, ni, par, trend):
     ll = gp.batch(th, hy)
     ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation.code, ds.t0,
                                th, hy)
-    _check(ll, ref, f"n{n}-np{np_}")
+    _check(ll, ref, f"n{n}-np{np_}", n)
     assert np.isfinite(ref).sum() >= 40
 
 
@@ -68,7 +69,7 @@ def test_gp_bjd_times():
                           rng.uniform(10, 40, 32)])
     ll = _gp(ds).batch(th, hy)
     ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th, hy)
-    _check(ll, ref, "bjd")
+    _check(ll, ref, "bjd", 200)
 
 
 def test_gp_config5_shape_and_paths():
@@ -89,7 +90,7 @@ def test_gp_config5_shape_and_paths():
     assert np.array_equal(out.cpu().numpy(), a, equal_nan=True)
     idx = np.r_[0:24, np.nonzero(~np.isfinite(a))[0][:8]]
     ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[idx], hy[idx])
-    _check(a[idx], ref, "config5")
+    _check(a[idx], ref, "config5", 512)
     assert (~np.isfinite(a)).sum() > 0
 
 
@@ -130,4 +131,4 @@ def test_gp_narrow_shape_matches(monkeypatch):
     fin = np.isfinite(base)
     assert np.max(np.abs(base[fin] - narrow[fin]) / np.abs(base[fin])) < 1e-4
     ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:16], hy[:16])
-    _check(narrow[:16], ref, "narrow")
+    _check(narrow[:16], ref, "narrow", 512)
