@@ -319,18 +319,13 @@ def config4_sharded_line(world: int, rank: int, backend: str, reps: int = 20) ->
             "bitwise_identical_to_single_gpu": same}
 
 
-def sampler_line(W: int, steps: int = 256) -> dict:
-    """Device-resident stretch move (rvk_stretch_run) on the config-2
-    posterior: ms per emcee step of W walkers (both halves: proposals, priors, likelihood,
-    accept/reject, chain write into HBM), HIP events on the launch stream; next to the host
-    stretch move driving the same posterior (numpy + LogPosterior.log_probability_batch)."""
+def _stretch_raw_ms(lpost, x0, steps: int, warm: int = 16, seed: int = 1234) -> tuple:
+    """ms per emcee step of rvk_stretch_run alone (state, draws and chain in HBM, no host copies),
+    HIP events on the launch stream; and the acceptance fraction."""
     import torch
     from ravest_amd import _lib
     from ravest_amd.posterior import DevicePosterior
-    from ravest_amd.sampler import EnsembleSampler
-    from ravest_amd.synth import make_posterior
-    lpost, x0 = make_posterior(2, W, device=torch.cuda.current_device())
-    D = x0.shape[1]
+    W, D = x0.shape
     dp = DevicePosterior(lpost)
     dev = torch.device("cuda", torch.cuda.current_device())
     x = torch.from_numpy(x0).to(dev)
@@ -344,25 +339,93 @@ def sampler_line(W: int, steps: int = 256) -> dict:
     st = torch.cuda.current_stream(dev)
 
     def run(n, step0):
-        _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, 1234, step0, 0, 0, 0, 0,
+        _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, seed, step0, 0, 0, 0, 0, 0,
                                      chain.data_ptr(), lnpc.data_ptr(), nacc.data_ptr(), status.data_ptr(),
                                      st.cuda_stream))
-    run(16, 0)
+    run(warm, 0)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(st)
-    run(steps, 16)
+    run(steps, warm)
     b.record(st)
     torch.cuda.synchronize(dev)
-    dev_ms = a.elapsed_time(b) / steps
-    acc = float(nacc.sum().item()) / ((steps + 16) * W)
+    acc = float(nacc.sum().item()) / ((steps + warm) * W)
+    if int(status.item()):
+        raise RuntimeError("NaN log-probability in the sampler benchmark")
+    return a.elapsed_time(b) / steps, acc
+
+
+def sampler_line(W: int, steps: int = 256, e2e_steps: int = 2048) -> dict:
+    """Device-resident stretch move on the config-2 posterior: (1) ms per emcee
+    step of rvk_stretch_run alone (proposals, priors, likelihood, accept/reject, chain into HBM;
+    emcee 3's randomised split drawn on the device); (2) the wall-clock a Fitter user sees:
+    DeviceEnsembleSampler.run_mcmc of e2e_steps steps from call to return, the chain and
+    log-probs landed in host memory (emcee's get_chain arrays); next to the host stretch move
+    driving the same posterior (numpy + LogPosterior.log_probability_batch)."""
+    import torch
+    from ravest_amd.sampler import DeviceEnsembleSampler, EnsembleSampler
+    from ravest_amd.synth import make_posterior
+    lpost, x0 = make_posterior(2, W, device=torch.cuda.current_device())
+    D = x0.shape[1]
+    dev_ms, acc = _stretch_raw_ms(lpost, x0, steps)
+    s = DeviceEnsembleSampler(lpost, W, seed=1234)
+    s.run_mcmc(x0, 2 * s.steps_per_call)                 # warm: buffers, pinned staging, graph capture
+    s.reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.run_mcmc(x0, e2e_steps)
+    e2e_ms = (time.perf_counter() - t0) / e2e_steps * 1e3
+    assert s.get_chain().shape == (e2e_steps, W, D)
     hs = EnsembleSampler(W, D, lpost.log_probability_batch, seed=1)
     hs.run_mcmc(x0, 2)
     t0 = time.perf_counter()
     hs.run_mcmc(x0, 20)
     host_ms = (time.perf_counter() - t0) / 20 * 1e3
     return {"what": f"device stretch move (rvk_stretch_run), config-2 posterior, {W} walkers, {D} free parameters, "
-                    "Philox draws, chain in HBM", "ms_per_step": dev_ms, "walker_steps_per_s": W / (dev_ms * 1e-3),
-            "acceptance": acc, "host_stretch_move_ms_per_step": host_ms, "speedup_vs_host": host_ms / dev_ms}
+                    "Philox draws with emcee 3's randomised split, chain in HBM", "ms_per_step": dev_ms,
+            "walker_steps_per_s": W / (dev_ms * 1e-3), "acceptance": acc,
+            "run_mcmc_e2e_ms_per_step": e2e_ms, "run_mcmc_e2e_over_kernel": e2e_ms / dev_ms,
+            "run_mcmc_e2e_note": f"DeviceEnsembleSampler.run_mcmc of {e2e_steps} steps, call to return, chain + "
+                                 f"log-probs in host memory ({s.steps_per_call}-step chunks copied out on a copy "
+                                 "stream while the next chunk runs)",
+            "host_stretch_move_ms_per_step": host_ms, "speedup_vs_host": host_ms / dev_ms}
+
+
+def config4_sampler_line(world: int, rank: int, backend: str, steps: int = 32) -> dict:
+    """Config 4 as a sampler: 65536 walkers (2 planets x 512 epochs, 14 free parameters).  N = 1:
+    DeviceEnsembleSampler's kernel (rvk_stretch_run, one fused kernel per half-step); N > 1:
+    ShardedDeviceSampler (each rank evaluates 32768 / N proposals per half-step, the 32768
+    log-posteriors all-gathered: 256 KB per half-step), run_mcmc timed with barriers, max over
+    ranks, chain kept on rank 0's host."""
+    import torch
+    import torch.distributed as dist
+    from ravest_amd.synth import make_posterior
+    W = 65536
+    lpost, x0 = make_posterior(4, W, device=torch.cuda.current_device())
+    D = x0.shape[1]
+    if world == 1:
+        ms, acc = _stretch_raw_ms(lpost, x0, steps, warm=4)
+        return {"what": f"config-4 posterior, {W} walkers, {D} free parameters, 1 GPU, rvk_stretch_run (chain in HBM)",
+                "ms_per_step": ms, "walker_steps_per_s": W / (ms * 1e-3),
+                "kepler_solves_per_s": W * 512 * 2 / (ms * 1e-3), "acceptance": acc}
+    if backend != "nccl":
+        return {"skipped": "gloo rehearsal: the sharded sampler's exchange is timed with RCCL only"}
+    from ravest_amd.distributed import ShardedDeviceSampler
+    s = ShardedDeviceSampler(lpost, W, seed=1234, steps_per_call=steps, keep_chain=0)
+    s.run_mcmc(x0, 4)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.run_mcmc(None, steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t[0]) / steps * 1e3
+    return {"what": f"config-4 posterior, {W} walkers, {D} free parameters, ShardedDeviceSampler over {world} GPUs "
+                    f"(RCCL all-gather of {W // 2} log-probs per half-step = {s.exchange_bytes_per_half_step} B)",
+            "ms_per_step": ms, "walker_steps_per_s": W / (ms * 1e-3), "kepler_solves_per_s": W * 512 * 2 / (ms * 1e-3),
+            "acceptance": float(s.acceptance_fraction.mean()), "n_gpus": world}
 
 
 def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
@@ -680,6 +743,10 @@ def main():
         c4 = config4_sharded_line(world, rank, backend)      # collective: every rank takes part
         if rank == 0:
             line["config4_sharded"] = c4
+    if not args.no_sampler:
+        c4s = config4_sampler_line(world, rank, backend)     # collective for N > 1
+        if rank == 0:
+            line["config4_sampler"] = c4s
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

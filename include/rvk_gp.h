@@ -111,7 +111,7 @@ int rvk_gp_logpost(rvk_gp_post *p, const double *free, int64_t n_walkers, int64_
  * draws and chain layout as rvk_stretch_run (include/rvk_post.h) -- per half-step the
  * proposals, rvk_gp_logpost_device on them, and the accept / reject, all stream-ordered. */
 int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t n_steps, double a,
-                       uint64_t seed, uint64_t step0, const int32_t *d_set, const double *d_zu,
+                       uint64_t seed, uint64_t step0, int32_t flags, const int32_t *d_set, const double *d_zu,
                        const int32_t *d_rint, const double *d_au, double *d_chain, double *d_lnp,
                        int64_t *d_naccepted, int32_t *d_status, void *stream);
 

@@ -82,6 +82,10 @@ int rvk_logpost_device(rvk_post *p, const double *d_free, int64_t n_walkers, int
                        double *d_out, void *stream);
 int rvk_logpost(rvk_post *p, const double *free, int64_t n_walkers, int64_t row_stride, double *out);
 
+/* RedBlueMove(randomize_split=False): the halves are the even / odd walkers (emcee 3.1's
+ * unshuffled `arange(W) % 2`).  Default (0): emcee's StretchMove, randomize_split=True. */
+#define RVK_STRETCH_FIXED_SPLIT 1
+
 /* Device-resident stretch move: n_steps emcee steps over the W-walker state
  * d_x[W][n_free] / d_lp[W] (updated in place; d_lp must hold the state's
  * log-posterior).  Per step, both halves in turn: proposals
@@ -89,33 +93,56 @@ int rvk_logpost(rvk_post *p, const double *free, int64_t n_walkers, int64_t row_
  * (n_free-1) log z + lp(q) - lp(s) > log(u').
  *
  * Random numbers:
- *   d_set == NULL: counter-based Philox4x32-10 keyed by `seed`, counter = step0
- *     + step; halves are walkers [0, W/2) and [W/2, W) (emcee 2's split).
+ *   d_set == NULL: counter-based Philox4x32-10 keyed by `seed`, counters = (global
+ *     step step0 + step, walker / proposal index).  The split is emcee 3's
+ *     randomize_split=True: per step a uniformly random balanced split of the W
+ *     walkers into two halves (each half's walkers ascending, as emcee's boolean
+ *     mask orders them); with RVK_STRETCH_FIXED_SPLIT the even / odd halves.  A
+ *     draw depends only on (seed, global step, half, proposal), so a run split
+ *     into several calls (step0 = steps done) is the same chain as one call.
  *   otherwise host-supplied draws for steps [0, n_steps), H = W/2, laid out
  *     [step][half][H]: d_set (walker indices of each half, ascending: emcee's
  *     shuffled `inds % 2` split), d_zu (u for z), d_rint (complement index in
  *     [0, H)), d_au (u' for the acceptance).  Drawn in emcee's call order these
- *     reproduce emcee's chain for the same seed.
+ *     reproduce emcee's chain for the same seed (flags ignored).
  * d_chain[n_steps][W][n_free] and d_lnp[n_steps][W] (either may be NULL) get
  * every step's state; d_naccepted[W] (int64, may be NULL) counts acceptances;
  * *d_status |= 1 if a NaN log-posterior was met (emcee raises ValueError).
  * Stream-ordered on `stream`. */
 int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t n_steps,
-                    double a, uint64_t seed, uint64_t step0, const int32_t *d_set,
+                    double a, uint64_t seed, uint64_t step0, int32_t flags, const int32_t *d_set,
                     const double *d_zu, const int32_t *d_rint, const double *d_au,
                     double *d_chain, double *d_lnp, int64_t *d_naccepted, int32_t *d_status,
                     void *stream);
 
-/* One half-step of the same stretch move over a SLICE of the active half's proposals
- * [j0, j0 + count) -- the multi-GPU form (ravest_amd.distributed.ShardedDeviceSampler): every
- * rank holds the whole state, makes and evaluates its slice of the proposals (Philox draws
- * keyed by the global proposal index and `step` = step0 + step, so the union over ranks is
- * the single-GPU half-step bit for bit), updates those walkers in d_x / d_lp and counts their
- * acceptances; the caller all-gathers the updated rows before the next half-step.  No chain
- * is written here.  Stream-ordered. */
-int rvk_stretch_half(rvk_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t half, int64_t j0,
-                     int64_t count, double a, uint64_t seed, uint64_t step, int64_t *d_naccepted,
-                     int32_t *d_status, void *stream);
+/* The same stretch move split for several GPUs (ravest_amd.distributed.ShardedDeviceSampler;
+ * ravest's pool.map over walkers, fit.py:1068-1075).  Every rank holds the whole state; per
+ * half-step each rank evaluates only a slice of the proposals, the H per-proposal
+ * log-posteriors are all-gathered (the one exchange: H doubles), and every rank applies the
+ * accept / reject to the whole half itself.  The chain equals rvk_stretch_run's bit for bit.
+ *
+ *   rvk_stretch_draws    the Philox draws of steps [step0, step0 + n_steps) into the
+ *                        posterior's draw table (same draws as rvk_stretch_run's);
+ *   rvk_stretch_propose  d_out[count] = log-posterior of proposals [j0, j0 + count) of
+ *                        (table step s, half) -- q = c - (c - s) z from the state d_x;
+ *   rvk_stretch_update   accept / reject of all W/2 proposals of (s, half) given their
+ *                        log-posteriors d_nlp[W/2]; updates d_x, d_lp; writes the half's
+ *                        walkers into d_chain_step[W][n_free] / d_lnp_step[W] (the step's
+ *                        chain rows; either may be NULL) and their acceptance counts
+ *                        d_nacc_out[w] = d_nacc_in[w] + accepted (equal pointers: a running
+ *                        count; separate ones: per-step counts; both may be NULL);
+ *                        *d_status |= 1 on NaN.
+ * Stream-ordered; rvk_stretch_run overwrites the draw table. */
+int rvk_stretch_draws(rvk_post *p, int64_t n_walkers, int32_t n_steps, double a, uint64_t seed, uint64_t step0,
+                      int32_t flags, void *stream);
+int rvk_stretch_propose(rvk_post *p, const double *d_x, int64_t n_walkers, int32_t s, int32_t half, int64_t j0,
+                        int64_t count, double *d_out, void *stream);
+/* Diagnostics: the drawn table's (walker, complement, z) of the W/2 proposals of (s, half), into
+ * host buffers (blocking; synchronises the device). */
+int rvk_stretch_table_read(rvk_post *p, int32_t s, int32_t half, int64_t *walker, int64_t *complement, double *z);
+int rvk_stretch_update(rvk_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t s, int32_t half,
+                       const double *d_nlp, double *d_chain_step, double *d_lnp_step, const int64_t *d_nacc_in,
+                       int64_t *d_nacc_out, int32_t *d_status, void *stream);
 
 #ifdef __cplusplus
 }

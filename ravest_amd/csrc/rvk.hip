@@ -132,8 +132,15 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                                                          long long stride, int wb, double *__restrict__ out,
                                                          PostArgs post, SampleArgs sa) {
     constexpr int WB = PassCfg<NP>::WB;
-    constexpr bool FUSE = SAMPLE == 2;
-    constexpr int WF = FUSE ? WB : 1;
+    // SAMPLE & 3: 1 accept / reject of propose_kernel's proposals; 2 proposals made in this kernel
+    // + accept / reject; 3 proposals made here, log-posterior out (rvk_stretch_propose).
+    // SAMPLE & 4 (EXT): every prior kind and the prior-side conversion in the fused prep (else the
+    // basic kinds only: no calls, the leaner register budget of the common posterior).
+    constexpr int MODE = SAMPLE & 3;
+    constexpr bool FUSE = MODE >= 2;
+    constexpr bool ACCEPT = MODE == 1 || MODE == 2;
+    constexpr bool EXT = (SAMPLE & 4) != 0;
+    constexpr int WF = FUSE ? BLK / 64 : 1;   // fused: one walker per wave per pass (launch_sample_fused)
     __shared__ PlanetK pks[WB][NP];
     __shared__ int okp[WB][NP];
     __shared__ double fq[WF][kFuseMaxD], fx[WF][kFuseMaxD], ff[WF][kFuseMaxPFull];
@@ -172,15 +179,14 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const RunArgs &run = *sa.run;
         const int D = sa.pd.n_free;
         const long long j = sa.j0 + w;   // global proposal index within the half
-        const PreDraw p = sa.pre ? sa.pre[((long long)sa.step * 2 + sa.half) * sa.hfull + j]
-                                 : make_pre(run, sa.step, sa.half, j, sa.hfull, D);
+        const PreDraw p = sa.pre[((long long)sa.step * 2 + sa.half) * sa.hfull + j];
         f.s = p.s;
         f.c = p.c;
         f.z = p.z;
         f.fac = p.fac;
         f.lau = p.lau;
-        f.lpo = run.lp[p.s];
-        f.nacc = run.nacc ? run.nacc[p.s] : 0;
+        f.lpo = ACCEPT ? run.lp[p.s] : 0.0;
+        f.nacc = (ACCEPT && run.nacc) ? run.nacc[p.s] : 0;
         f.a = f.b = 0.0;
         if (lane < D) {
             f.a = run.x[p.s * D + lane];
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             // SAMPLE: the accept test's operands are loaded before the epoch loop, so their latency
             // (sidx -> lp[sidx] is a dependent pair) hides under the loop instead of the wave's tail
             long long sw_s = 0, nacc_s = 0;
-            double lp_old_s = 0.0, fac_s = 0.0, au_s = 1.0, lau_s = 0.0;
+            double lp_old_s = 0.0, fac_s = 0.0, lau_s = 0.0;
             if constexpr (FUSE) {   // this wave's proposal (StretchMove.get_proposal + fit.py:3461-3482)
                 // Lane-parallel and register-resident: lane c < D holds q_c, lane k < p_full the
                 // full row's column k (a ds_bpermute of q), lane k < n_prior its prior term; only
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 const int D = pd.n_free;
                 const Fetch f = (base == (long long)blockIdx.x * wb && j == wv) ? pre : fetch(w);
                 lp_old_s = f.lpo;                         // (needed only in the epilogue)
-                const double q_s = lane < D ? f.b - (f.b - f.a) * f.z : 0.0;
+                const double q_s = lane < D ? stretch_q(f.b, f.a, f.z) : 0.0;
                 if (lane < D) {                           // parked for the epilogue (read back by the same lane)
                     fq[j][lane] = q_s;
                     fx[j][lane] = f.a;
@@ -249,21 +255,32 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 }
                 const int ioff = 5 * pd.n_planets + pd.n_inst;
                 const double jv = shfl_d(fv, ioff + (lane < pd.n_inst ? lane : 0));
-                const bool dead0 = lane < pd.n_inst && jv < 0.0;                              // fit.py:3465-3468
+                bool dead0 = lane < pd.n_inst && jv < 0.0;                                    // fit.py:3465-3468
                 double term = 0.0;
-                {
-                    const int src = lane < pd.n_prior ? fsl[lane].src : 0;
-                    const double xv = shfl_d(fv, src);
-                    if (lane < pd.n_prior) {
-                        const PriorSlot &sl = fsl[lane];
-                        term = prior_lp_basic(sl.kind, sl.p, xv);
-                    }
-                }
                 {
                     const int pl = lane < NP ? lane : 0;
                     double p5[5];
 #pragma unroll
                     for (int k = 0; k < 5; ++k) p5[k] = shfl_d(fv, 5 * pl + k);
+                    // the prior-side conversion (Case 3, fit.py:3418-3446): lane p < NP converts
+                    // planet p; a ValueError rejects the walker; a slot with src < 0 reads it
+                    const int src = lane < pd.n_prior ? fsl[lane].src : 0;
+                    double xv = shfl_d(fv, src < 0 ? 0 : src);
+                    if constexpr (EXT) {
+                        double d5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                        if (pd.convert && lane < NP) dead0 |= !to_default_call(pd.par, p5, d5);
+                        if (pd.convert) {                 // wave-uniform branch
+                            const int di = src < 0 ? -src - 1 : 0, dp = di / 5, dj = di - 5 * dp;
+#pragma unroll
+                            for (int k = 0; k < 5; ++k) {
+                                const double v = shfl_d(d5[k], dp);
+                                if (src < 0 && dj == k) xv = v;
+                            }
+                        }
+                        if (lane < pd.n_prior) term = prior_lp(fsl[lane], xv);
+                    } else {
+                        if (lane < pd.n_prior) term = prior_lp_basic(fsl[lane].kind, fsl[lane].p, xv);
+                    }
                     if (lane < NP) {
                         PlanetK pk;
                         const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
@@ -293,7 +310,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 // epoch loop's LDS reads wait on)
                 lp_old_s = *(const __attribute__((address_space(1))) double *)(sa.run->lp + sw_s);
                 fac_s = sa.fac[w];
-                au_s = sa.au[w];
+                lau_s = sa.lau[w];
             }
             bool all_ok = true;
 #pragma unroll
@@ -400,12 +417,12 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
             if (FUSE || post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
             }
-            if constexpr (SAMPLE != 0) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
+            if constexpr (ACCEPT) {   // RedBlueMove: accept if (ndim-1) log z + lp(q) - lp(s) > log u'
                 const RunArgs &run = *sa.run;
                 const int D = sa.D;
                 const long long sw = sw_s;
                 const double lp_old = lp_old_s;
-                const bool acc = fac_s + res - lp_old > (FUSE ? lau_s : log(au_s));
+                const bool acc = stretch_accept(fac_s, res, lp_old, lau_s);
                 double *xs = run.x + sw * D;
                 const long long W2 = 2 * sa.hfull;
                 double *chain = run.chain ? run.chain + (long long)sa.step * W2 * D : nullptr;
@@ -432,7 +449,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     if (run.lnpc) run.lnpc[(long long)sa.step * W2 + sw] = acc ? res : lp_old;
                 }
             } else {
-                if (lane == 0) out[w] = res;
+                if (lane == 0) (MODE == 3 ? sa.out : out)[w] = res;
                 LL_MARK(6);
             }
         }
@@ -730,14 +747,16 @@ void launch_sample(hipStream_t st, EpochData d, int n, int ni, const double *row
                        ni, rows, H, stride, wb, nullptr, post, sa);
 }
 
-// The same with the proposals made in the kernel's prep (SAMPLE == 2; rows unused).
-template <int NP, bool MULTI, bool TP>
+// The same with the proposals made in the kernel's prep (SAMPLE == 2; rows unused), or only the
+// proposals' log-posteriors (SAMPLE == 3, rvk_stretch_propose).
+template <int NP, bool MULTI, bool TP, int SAMPLE>
 void launch_sample_fused(hipStream_t st, EpochData d, int n, int ni, const double *rows, long long H, long long stride,
                          PostArgs post, const SampleArgs &sa) {
-    long long blocks;
-    int wb;
-    ll_grid<NP>(H, blocks, wb, RVK_SAMPLE_BLOCK / 64);
-    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, 2, RVK_SAMPLE_BLOCK>), dim3((unsigned)blocks),
+    // one walker per wave per pass (the kernel's fused LDS rows are per wave); grid-stride beyond
+    constexpr int wb = RVK_SAMPLE_BLOCK / 64;
+    long long blocks = (H + wb - 1) / wb;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((loglike_kernel<NP, MULTI, 0, TP, SAMPLE, RVK_SAMPLE_BLOCK>), dim3((unsigned)blocks),
                        dim3(RVK_SAMPLE_BLOCK), 0, st, d, n, ni, rows, H, stride, wb, nullptr, post, sa);
 }
 
@@ -766,25 +785,38 @@ loglike_launch_t pick_ll(int np, bool multi, int solver, bool tp) {
     return tp ? pick_ll_t<0, true>(np, multi) : pick_ll_t<0, false>(np, multi);
 }
 
-template <bool MULTI, bool TP, bool FUSED>
+// MODE 1: propose_kernel + the likelihood with the accept / reject; 2: one fused half-step;
+// 3: fused proposals, log-posterior out (the fused modes: NP <= 4); | 4: every prior kind and
+// the prior-side conversion in the fused prep.
+template <bool MULTI, bool TP, int MODE>
 sample_launch_t pick_sample_s(int np) {
-    switch (np) {
-        case 1: return FUSED ? launch_sample_fused<1, MULTI, TP> : launch_sample<1, MULTI, TP>;
-        case 2: return FUSED ? launch_sample_fused<2, MULTI, TP> : launch_sample<2, MULTI, TP>;
-        case 3: return FUSED ? launch_sample_fused<3, MULTI, TP> : launch_sample<3, MULTI, TP>;
-        case 4: return FUSED ? launch_sample_fused<4, MULTI, TP> : launch_sample<4, MULTI, TP>;
-        case 5: return FUSED ? nullptr : launch_sample<5, MULTI, TP>;   // (fused: NP <= 4)
-        case 6: return FUSED ? nullptr : launch_sample<6, MULTI, TP>;   // (fused: NP <= 4)
-        case 7: return FUSED ? nullptr : launch_sample<7, MULTI, TP>;   // (fused: NP <= 4)
-        case 8: return FUSED ? nullptr : launch_sample<8, MULTI, TP>;   // (fused: NP <= 4)
-        default: return nullptr;
+    if constexpr (MODE == 1) {
+        switch (np) {
+            case 1: return launch_sample<1, MULTI, TP>;
+            case 2: return launch_sample<2, MULTI, TP>;
+            case 3: return launch_sample<3, MULTI, TP>;
+            case 4: return launch_sample<4, MULTI, TP>;
+            case 5: return launch_sample<5, MULTI, TP>;
+            case 6: return launch_sample<6, MULTI, TP>;
+            case 7: return launch_sample<7, MULTI, TP>;
+            case 8: return launch_sample<8, MULTI, TP>;
+            default: return nullptr;
+        }
+    } else {
+        switch (np) {
+            case 1: return launch_sample_fused<1, MULTI, TP, MODE>;
+            case 2: return launch_sample_fused<2, MULTI, TP, MODE>;
+            case 3: return launch_sample_fused<3, MULTI, TP, MODE>;
+            case 4: return launch_sample_fused<4, MULTI, TP, MODE>;
+            default: return nullptr;
+        }
     }
 }
 
-template <bool FUSED>
+template <int MODE>
 sample_launch_t pick_sample(int np, bool multi, bool tp) {
-    if (multi) return tp ? pick_sample_s<true, true, FUSED>(np) : pick_sample_s<true, false, FUSED>(np);
-    return tp ? pick_sample_s<false, true, FUSED>(np) : pick_sample_s<false, false, FUSED>(np);
+    if (multi) return tp ? pick_sample_s<true, true, MODE>(np) : pick_sample_s<true, false, MODE>(np);
+    return tp ? pick_sample_s<false, true, MODE>(np) : pick_sample_s<false, false, MODE>(np);
 }
 
 int check_gfx950(int dev) {
@@ -918,8 +950,11 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->par = par;
     h->t0 = t0;
     h->launch = pick_ll(n_planets, n_inst > 1, 0, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample = pick_sample<false>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_fused = pick_sample<true>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample = pick_sample<1>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_fused[0] = pick_sample<2>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_eval[0] = pick_sample<3>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_fused[1] = pick_sample<6>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_eval[1] = pick_sample<7>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;

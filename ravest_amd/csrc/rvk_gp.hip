@@ -912,21 +912,21 @@ __global__ __launch_bounds__(256) void gp_logprior_kernel(PostDev pd, int n_lp, 
 }
 
 // Stretch-move proposals of one half for the GP sampler (emcee StretchMove.get_proposal), one
-// thread per proposal: q = c - (c - s) z, z = ((a - 1) u + 1)^2 / a; the log-posterior of the
-// block of proposals is then rvk_gp_logpost_device, the accept / reject stretch_accept_kernel.
-__global__ __launch_bounds__(256) void gp_propose_kernel(const RunArgs *__restrict__ runp, int D, int step, int half,
-                                                         long long H, double *__restrict__ q, double *__restrict__ fac,
-                                                         double *__restrict__ au, long long *__restrict__ sidx) {
+// thread per proposal: q = c - (c - s) z with the draws of (step, half, j) from `pre`; the
+// log-posterior of the block of proposals is then rvk_gp_logpost_device, the accept / reject
+// stretch_accept_kernel.
+__global__ __launch_bounds__(256) void gp_propose_kernel(const RunArgs *__restrict__ runp, const PreDraw *__restrict__ pre,
+                                                         int D, int step, int half, long long H, double *__restrict__ q,
+                                                         double *__restrict__ fac, double *__restrict__ lau,
+                                                         long long *__restrict__ sidx) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= H) return;
     const RunArgs &run = *runp;
-    const Draw d = draw(run, step, half, j, H);
-    const double zt = (run.a - 1.0) * d.zu + 1.0;
-    const double z = zt * zt / run.a;
+    const PreDraw d = pre[((long long)step * 2 + half) * H + j];
     const double *xs = run.x + d.s * D, *xc = run.x + d.c * D;
-    for (int c = 0; c < D; ++c) q[j * D + c] = xc[c] - (xc[c] - xs[c]) * z;
-    fac[j] = ((double)D - 1.0) * log(z);
-    au[j] = d.au;
+    for (int c = 0; c < D; ++c) q[j * D + c] = stretch_q(xc[c], xs[c], d.z);
+    fac[j] = d.fac;
+    lau[j] = d.lau;
     sidx[j] = d.s;
 }
 
@@ -1176,9 +1176,11 @@ struct rvk_gp_post {
     double *d_full = nullptr, *d_lp = nullptr, *d_lhp = nullptr;   // workspace for capw walkers
     // rvk_gp_stretch_run: proposals of a half, their log-posteriors, per-chunk arguments
     long long caph = 0;
-    double *d_q = nullptr, *d_fac = nullptr, *d_au = nullptr, *d_nlp = nullptr;
+    double *d_q = nullptr, *d_fac = nullptr, *d_lau = nullptr, *d_nlp = nullptr;
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;
+    PreDraw *d_pre = nullptr;      // [kStepsPerGraph][2][caph] the chunk's draws
+    DrawTable tab;                 // device draws of a block of steps
     double *d_xin = nullptr, *d_oin = nullptr;                     // rvk_gp_logpost's staging
     size_t cap_xin = 0, cap_oin = 0;
 
@@ -1201,10 +1203,12 @@ static void free_gp_post(rvk_gp_post *p) {
     (void)hipFree(p->d_oin);
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
-    (void)hipFree(p->d_au);
+    (void)hipFree(p->d_lau);
     (void)hipFree(p->d_nlp);
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
+    (void)hipFree(p->d_pre);
+    p->tab.release();
     delete p;
 }
 
@@ -1213,15 +1217,18 @@ static int gp_post_reserve_half(rvk_gp_post *p, long long H) {
     HIPCHK(hipSetDevice(p->g->h->device));
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
-    (void)hipFree(p->d_au);
+    (void)hipFree(p->d_lau);
     (void)hipFree(p->d_nlp);
     (void)hipFree(p->d_sidx);
-    p->d_q = p->d_fac = p->d_au = p->d_nlp = nullptr;
+    (void)hipFree(p->d_pre);
+    p->d_q = p->d_fac = p->d_lau = p->d_nlp = nullptr;
     p->d_sidx = nullptr;
+    p->d_pre = nullptr;
     p->caph = 0;
     HIPCHK(hipMalloc(&p->d_q, sizeof(double) * (size_t)H * (size_t)p->n_free));
     HIPCHK(hipMalloc(&p->d_fac, sizeof(double) * (size_t)H));
-    HIPCHK(hipMalloc(&p->d_au, sizeof(double) * (size_t)H));
+    HIPCHK(hipMalloc(&p->d_lau, sizeof(double) * (size_t)H));
+    HIPCHK(hipMalloc(&p->d_pre, sizeof(PreDraw) * (size_t)kStepsPerGraph * 2 * (size_t)H));
     HIPCHK(hipMalloc(&p->d_nlp, sizeof(double) * (size_t)H));
     HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * (size_t)H));
     if (!p->d_run) HIPCHK(hipMalloc(&p->d_run, sizeof(RunArgs)));
@@ -1356,13 +1363,14 @@ int rvk_gp_logpost(rvk_gp_post *p, const double *xf, int64_t W, int64_t stride, 
 }
 
 int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t W, int32_t n_steps, double a, uint64_t seed,
-                       uint64_t step0, const int32_t *d_set, const double *d_zu, const int32_t *d_rint,
+                       uint64_t step0, int32_t flags, const int32_t *d_set, const double *d_zu, const int32_t *d_rint,
                        const double *d_au, double *d_chain, double *d_lnp, int64_t *d_naccepted, int32_t *d_status,
                        void *stream) {
     if (!p) return fail(RVK_E_ARG, "NULL GP posterior");
     if (W < 4 || (W & 1)) return fail(RVK_E_ARG, "n_walkers must be even and >= 4");
     if (n_steps < 0) return fail(RVK_E_ARG, "n_steps < 0");
     if (!(a > 1.0)) return fail(RVK_E_ARG, "stretch scale a must be > 1");
+    if (flags & ~RVK_STRETCH_FIXED_SPLIT) return fail(RVK_E_ARG, "unknown flags");
     if (!d_x || !d_lp || !d_status) return fail(RVK_E_ARG, "NULL device buffer");
     if (d_set && (!d_zu || !d_rint || !d_au)) return fail(RVK_E_ARG, "host draws need set, zu, rint and au");
     if (n_steps == 0) return RVK_OK;
@@ -1373,32 +1381,38 @@ int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t W, int
     HIPCHK(hipSetDevice(p->g->h->device));
     const int D = p->n_free;
     const size_t wd = (size_t)W * (size_t)D, hh = 2 * (size_t)H;
-    constexpr int kChunk = 8;
-    for (int s0 = 0; s0 < n_steps; s0 += kChunk) {
-        const int n = (n_steps - s0) < kChunk ? (n_steps - s0) : kChunk;
-        RunArgs run{d_x,
-                    d_lp,
-                    (long long *)d_naccepted,
-                    (int *)d_status,
-                    d_chain ? d_chain + (size_t)s0 * wd : nullptr,
-                    d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
-                    d_set ? d_set + (size_t)s0 * hh : nullptr,
-                    d_set ? d_zu + (size_t)s0 * hh : nullptr,
-                    d_set ? d_rint + (size_t)s0 * hh : nullptr,
-                    d_set ? d_au + (size_t)s0 * hh : nullptr,
-                    seed,
-                    step0 + (uint64_t)s0,
-                    a};
-        hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
-        const unsigned blocks = (unsigned)((H + 255) / 256);
-        for (int s = 0; s < n; ++s)
-            for (int half = 0; half < 2; ++half) {
-                hipLaunchKernelGGL(gp_propose_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, D, s, half, H, p->d_q,
-                                   p->d_fac, p->d_au, p->d_sidx);
-                if ((rc = rvk_gp_logpost_device(p, p->d_q, H, D, p->d_nlp, st))) return rc;
-                hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, s, H, D, p->d_q,
-                                   p->d_fac, p->d_au, p->d_sidx, p->d_nlp);
-            }
+    const unsigned blocks = (unsigned)((H + 255) / 256);
+    const int blk = d_set ? n_steps : draws_block_steps(H);
+    for (int b0 = 0; b0 < n_steps; b0 += blk) {
+        const int nb = (n_steps - b0) < blk ? (n_steps - b0) : blk;
+        if (!d_set && (rc = draws_fill(p->tab, st, H, nb, D, seed, step0 + (uint64_t)b0, a, flags))) return rc;
+        for (int s0 = b0; s0 < b0 + nb; s0 += kStepsPerGraph) {
+            const int n = (b0 + nb - s0) < kStepsPerGraph ? (b0 + nb - s0) : kStepsPerGraph;
+            RunArgs run{d_x,
+                        d_lp,
+                        (long long *)d_naccepted,
+                        (int *)d_status,
+                        d_chain ? d_chain + (size_t)s0 * wd : nullptr,
+                        d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
+                        d_set ? d_set + (size_t)s0 * hh : nullptr,
+                        d_set ? d_zu + (size_t)s0 * hh : nullptr,
+                        d_set ? d_rint + (size_t)s0 * hh : nullptr,
+                        d_set ? d_au + (size_t)s0 * hh : nullptr,
+                        seed,
+                        step0 + (uint64_t)s0,
+                        a};
+            const long long np = (long long)n * 2 * H;
+            hipLaunchKernelGGL(chunk_args_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, p->d_run, run,
+                               p->d_pre, d_set ? nullptr : p->tab.block + (size_t)(s0 - b0) * hh, n, H, D);
+            for (int s = 0; s < n; ++s)
+                for (int half = 0; half < 2; ++half) {
+                    hipLaunchKernelGGL(gp_propose_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, p->d_pre, D, s,
+                                       half, H, p->d_q, p->d_fac, p->d_lau, p->d_sidx);
+                    if ((rc = rvk_gp_logpost_device(p, p->d_q, H, D, p->d_nlp, st))) return rc;
+                    hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, s, H, D,
+                                       p->d_q, p->d_fac, p->d_lau, p->d_sidx, p->d_nlp);
+                }
+        }
     }
     HIPCHK(hipGetLastError());
     return RVK_OK;

@@ -54,6 +54,27 @@ int grow_dev(void **p, size_t *cap, size_t need);
 // Per-device copy of the sin/cos table, uploaded once per process (never freed).
 int shared_table(int device, const SC **tab);
 
+// Steps per cached graph replay of the device stretch move (and per chunk_args_kernel).
+constexpr int kStepsPerGraph = 8;
+
+// The stretch move's device draws (split_draws_kernel) for a block of steps: table[s][half][j]
+// for steps step0 .. step0 + steps - 1, plus the kernel's scratch.  Owned by a posterior.
+struct DrawTable {
+    PreDraw *block = nullptr;
+    uint32_t *keys = nullptr;
+    int32_t *sets = nullptr;
+    size_t cap_block = 0, cap_keys = 0, cap_sets = 0;   // bytes
+    long long H = 0;                                     // walkers per half of the current content
+    int steps = 0;
+    void release();
+};
+
+// Fill `t` with the draws of n_steps steps from global step step0 (RVK_STRETCH_* flags), stream-ordered.
+int draws_fill(DrawTable &t, hipStream_t st, long long H, int n_steps, int D, uint64_t seed, uint64_t step0, double a,
+               int flags);
+// Steps per draw block for H walkers per half: a multiple of kStepsPerGraph, table <= 256 MB.
+int draws_block_steps(long long H);
+
 }  // namespace rvk
 
 // As HIPCHK, but first drains `stream`, so no async copy into a caller's buffer is still in
@@ -88,7 +109,10 @@ struct rvk_handle {
     size_t cap_theta = 0, cap_out = 0, cap_tq = 0, cap_iq = 0;
     rvk::loglike_launch_t launch = nullptr;
     rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
-    rvk::sample_launch_t sample_fused = nullptr;   // ... with the proposals made in the same kernel
+    // ... with the proposals made in the same kernel, and proposals + log-posterior only
+    // (rvk_stretch_propose); [1]: every prior kind and the prior-side conversion in the prep
+    rvk::sample_launch_t sample_fused[2] = {nullptr, nullptr};
+    rvk::sample_launch_t sample_eval[2] = {nullptr, nullptr};
     int solver = 0;
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW

@@ -39,38 +39,35 @@ __global__ __launch_bounds__(256) void logprior_kernel(PostDev pd, const double 
 }
 
 // Stretch-move proposals of one half (emcee StretchMove.get_proposal), one wave per
-// proposal: q = c - (c - s) * z, z = ((a - 1) u + 1)^2 / a, factor = (ndim - 1) log z;
-// then its full row and log-prior.  The accept / reject runs in the epilogue of the
-// log-likelihood kernel (SAMPLE mode) or in accept_kernel.
-__global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs *__restrict__ runp, int step,
-                                                      int half, long long H, long long j0, long long hfull,
-                                                      double *__restrict__ q,
-                                                      double *__restrict__ full,
-                                                      double *__restrict__ lp, double *__restrict__ fac,
-                                                      double *__restrict__ au, long long *__restrict__ sidx) {
+// proposal: q = c - (c - s) z with the draws of (step, half, j0 + j) from `pre`; then its full
+// row and log-prior.  The accept / reject runs in the epilogue of the log-likelihood kernel
+// (SAMPLE mode) or in stretch_accept_kernel.
+__global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs *__restrict__ runp,
+                                                      const PreDraw *__restrict__ pre, int step, int half, long long H,
+                                                      long long j0, long long hfull, double *__restrict__ q,
+                                                      double *__restrict__ full, double *__restrict__ lp,
+                                                      double *__restrict__ fac, double *__restrict__ lau,
+                                                      long long *__restrict__ sidx) {
     __shared__ PostWaveLds lds[kWavesPerBlock];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PostWaveLds &L = lds[wv];
     const int D = pd.n_free;
-    const RunArgs &run = *runp;
-    const double *x = run.x, a = run.a;
-    const RowPre pre = row_pre(pd);
+    const double *x = runp->x;
+    const RowPre rp = row_pre(pd);
     for (long long j = (long long)blockIdx.x * kWavesPerBlock + wv; j < H; j += (long long)gridDim.x * kWavesPerBlock) {
-        const Draw d = draw(run, step, half, j0 + j, hfull);   // proposal j0 + j of the half
-        const double zt = (a - 1.0) * d.zu + 1.0;
-        const double z = zt * zt / a;
+        const PreDraw d = pre[((long long)step * 2 + half) * hfull + j0 + j];   // proposal j0 + j of the half
         const double *xs = x + d.s * D, *xc = x + d.c * D;
         for (int c = lane; c < D; c += 64) {
-            const double v = xc[c] - (xc[c] - xs[c]) * z;
+            const double v = stretch_q(xc[c], xs[c], d.z);
             L.x[c] = v;
             q[j * D + c] = v;
         }
         wave_lds_sync();
-        const double v = post_row_wave(pd, L, full + j * pd.p_full, pre);
+        const double v = post_row_wave(pd, L, full + j * pd.p_full, rp);
         if (lane == 0) {
             lp[j] = v;
-            fac[j] = ((double)D - 1.0) * log(z);
-            au[j] = d.au;
+            fac[j] = d.fac;
+            lau[j] = d.lau;
             sidx[j] = d.s;
         }
         wave_lds_sync();
@@ -78,8 +75,6 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs 
 }
 
 unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
-
-constexpr int kStepsPerGraph = 8;   // steps per cached graph replay (4 or 6 kernels each)
 
 // one wave per item, at most 2^16 blocks (grid-stride beyond)
 unsigned wave_blocks(long long n) {
@@ -94,16 +89,19 @@ struct rvk_post {
     int n_free = 0, n_prior = 0;
     bool convert = false;
     bool fusable = false;                  // proposals can be made inside the likelihood kernel
+    int ext = 0;                           // ... with a transcendental prior kind or the conversion
     double jac = 0.0, renorm = 0.0;
     int32_t *d_colmap = nullptr;
     double *d_tmpl = nullptr;
     PriorSlot *d_slots = nullptr;
     // workspace, sized for cap walkers
     long long capw = 0;
-    double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_au = nullptr;
+    double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_lau = nullptr;
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;              // rvk_stretch_run's per-chunk arguments
-    PreDraw *d_pre = nullptr;              // [kStepsPerGraph][2][capw] the chunk's draws (fused path)
+    PreDraw *d_pre = nullptr;              // [kStepsPerGraph][2][caph] the chunk's draws (fixed address)
+    long long caph = 0;
+    DrawTable tab;                         // device draws of a block of steps (split_draws_kernel)
     double *d_xin = nullptr, *d_oin = nullptr;   // rvk_logpost's host-buffer staging, grown on demand
     size_t cap_xin = 0, cap_oin = 0;
     hipStream_t cap = nullptr;             // capture stream
@@ -118,41 +116,40 @@ struct rvk_post {
 };
 
 // Kernels of one half-step over proposals [j0, j0 + count) of a half of hfull walkers, reading
-// this chunk's RunArgs (p->d_run): propose, then the likelihood with the accept / reject fused in
-// (production solver), or both in one kernel (fused path), or the likelihood and accept_kernel
-// (reference solver).
+// this chunk's RunArgs (p->d_run) and draws `pre` ([steps][2][hfull]): the proposals made and
+// accepted inside the likelihood kernel (fused path), or propose_kernel + the likelihood with
+// the accept / reject fused in (production solver), or + stretch_accept_kernel (reference solver).
 static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long j0, long long count,
                          long long hfull, const PreDraw *pre) {
     rvk_handle *h = p->h;
     const PostDev pd = p->dev();
     const PostArgs post{p->d_lp, p->jac, p->renorm};
-    const bool fused = p->fusable && h->solver == 0 && h->sample_fused;
+    const bool fused = p->fusable && h->solver == 0 && h->sample_fused[p->ext];
     const long long H = count;
     if (fused) {
-        const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, hfull, pre};
-        h->sample_fused(st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
+        const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, hfull, pre,
+                            nullptr};
+        h->sample_fused[p->ext](st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
         return;
     }
-    hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, s, half, H, j0, hfull,
-                       p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_au, p->d_sidx);
+    hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(H)), dim3(256), 0, st, pd, p->d_run, pre, s, half, H, j0, hfull,
+                       p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_lau, p->d_sidx);
     if (h->solver == 0 && h->sample) {
-        const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_run, s, half, pd, j0, hfull, nullptr};
+        const SampleArgs sa{p->n_free, p->d_q, p->d_fac, p->d_lau, p->d_sidx, p->d_run, s, half, pd, j0, hfull, pre,
+                            nullptr};
         h->sample(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), post, sa);
     } else {
         h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, H, h->p_full(), p->d_nlp, post);
         hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks_for(H)), dim3(256), 0, st, p->d_run, s, H, p->n_free,
-                           p->d_q, p->d_fac, p->d_au, p->d_sidx, p->d_nlp);
+                           p->d_q, p->d_fac, p->d_lau, p->d_sidx, p->d_nlp);
     }
 }
 
-// Kernels of n steps (both halves, all proposals) reading this chunk's RunArgs.
+// Kernels of n steps (both halves, all proposals) reading this chunk's RunArgs and draws.
 static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
     for (int s = 0; s < n; ++s)
         for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H, p->d_pre);
 }
-
-// The fused half-step takes its draws from a per-chunk table when there is one.
-static bool uses_pre(const rvk_post *p) { return p->fusable && p->h->solver == 0 && p->h->sample_fused; }
 
 // The kStepsPerGraph-step chunk as a HIP graph, captured once per (H, solver) and
 // replayed: its kernel arguments never change (everything per call is in d_run).
@@ -187,10 +184,11 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
     (void)hipFree(p->d_nlp);
-    (void)hipFree(p->d_au);
+    (void)hipFree(p->d_lau);
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
     (void)hipFree(p->d_pre);
+    p->tab.release();
     (void)hipFree(p->d_xin);
     (void)hipFree(p->d_oin);
     if (p->graph) (void)hipGraphExecDestroy(p->graph);
@@ -208,12 +206,10 @@ static int reserve_impl(rvk_post *p, long long W) {
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
     (void)hipFree(p->d_nlp);
-    (void)hipFree(p->d_au);
+    (void)hipFree(p->d_lau);
     (void)hipFree(p->d_sidx);
-    (void)hipFree(p->d_pre);
-    p->d_full = p->d_lp = p->d_q = p->d_fac = p->d_nlp = p->d_au = nullptr;
+    p->d_full = p->d_lp = p->d_q = p->d_fac = p->d_nlp = p->d_lau = nullptr;
     p->d_sidx = nullptr;
-    p->d_pre = nullptr;
     p->capw = 0;
     const size_t w = (size_t)W;
     HIPCHK(hipMalloc(&p->d_full, sizeof(double) * w * (size_t)p->h->p_full()));
@@ -221,10 +217,23 @@ static int reserve_impl(rvk_post *p, long long W) {
     HIPCHK(hipMalloc(&p->d_q, sizeof(double) * w * (size_t)(p->n_free > 0 ? p->n_free : 1)));
     HIPCHK(hipMalloc(&p->d_fac, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_nlp, sizeof(double) * w));
-    HIPCHK(hipMalloc(&p->d_au, sizeof(double) * w));
+    HIPCHK(hipMalloc(&p->d_lau, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * w));
-    if (p->fusable) HIPCHK(hipMalloc(&p->d_pre, sizeof(PreDraw) * (size_t)kStepsPerGraph * 2 * w));
     p->capw = W;
+    return RVK_OK;
+}
+
+// The chunk's draw region for H walkers per half (the graph reads it at a fixed address).
+static int reserve_chunk(rvk_post *p, long long H) {
+    if (H <= p->caph) return RVK_OK;
+    if (p->graph) (void)hipGraphExecDestroy(p->graph);
+    p->graph = nullptr;
+    HIPCHK(hipSetDevice(p->h->device));
+    (void)hipFree(p->d_pre);
+    p->d_pre = nullptr;
+    p->caph = 0;
+    HIPCHK(hipMalloc(&p->d_pre, sizeof(PreDraw) * (size_t)kStepsPerGraph * 2 * (size_t)H));
+    p->caph = H;
     return RVK_OK;
 }
 
@@ -258,14 +267,14 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
     p->n_free = n_free;
     p->n_prior = n_prior;
     p->convert = convert;
-    // The fused sampler path (loglike_kernel SAMPLE == 2) stages a walker's proposal and full
-    // row in LDS and evaluates the basic prior kinds inline; RVK_SAMPLER_FUSE=0 (experiment
+    // The fused sampler path (loglike_kernel SAMPLE >= 2) makes a walker's proposal, full row,
+    // conversion and priors lane-parallel in the walker's wave; RVK_SAMPLER_FUSE=0 (experiment
     // hook) keeps the two-kernel path.
+    const char *fe = getenv("RVK_SAMPLER_FUSE");
+    p->fusable = n_free <= kFuseMaxD && pf <= kFuseMaxPFull && n_prior <= kFuseMaxPrior && !(fe && atoi(fe) == 0);
     bool basic = true;
     for (int k = 0; k < n_prior; ++k) basic &= kind[k] <= kMaxBasicPriorKind;
-    const char *fe = getenv("RVK_SAMPLER_FUSE");
-    p->fusable = basic && !convert && n_free <= kFuseMaxD && pf <= kFuseMaxPFull && n_prior <= kFuseMaxPrior &&
-                 !(fe && atoi(fe) == 0);
+    p->ext = (basic && !convert) ? 0 : 1;
     p->jac = jac;
     p->renorm = renorm;
     HIPCHK(hipSetDevice(h->device));
@@ -277,6 +286,42 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
     HIPCHK(hipMemcpy(p->d_tmpl, tmpl, sizeof(double) * pf, hipMemcpyHostToDevice));
     if (n_prior > 0)
         HIPCHK(hipMemcpy(p->d_slots, slots.data(), sizeof(PriorSlot) * n_prior, hipMemcpyHostToDevice));
+    return RVK_OK;
+}
+
+void rvk::DrawTable::release() {
+    (void)hipFree(block);
+    (void)hipFree(keys);
+    (void)hipFree(sets);
+    block = nullptr;
+    keys = nullptr;
+    sets = nullptr;
+    cap_block = cap_keys = cap_sets = 0;
+    H = 0;
+    steps = 0;
+}
+
+int rvk::draws_block_steps(long long H) {
+    const long long per = 2 * H * (long long)(sizeof(PreDraw) + 8);      // table + scratch per step
+    long long n = (256LL << 20) / (per > 0 ? per : 1);
+    if (n > 256) n = 256;
+    n -= n % kStepsPerGraph;
+    return (int)(n < kStepsPerGraph ? kStepsPerGraph : n);
+}
+
+int rvk::draws_fill(DrawTable &t, hipStream_t st, long long H, int n_steps, int D, uint64_t seed, uint64_t step0,
+                    double a, int flags) {
+    const size_t W = 2 * (size_t)H, n = (size_t)n_steps;
+    int rc;
+    if ((rc = grow_dev((void **)&t.block, &t.cap_block, sizeof(PreDraw) * W * n)) ||
+        (rc = grow_dev((void **)&t.keys, &t.cap_keys, sizeof(uint32_t) * W * n)) ||
+        (rc = grow_dev((void **)&t.sets, &t.cap_sets, sizeof(int32_t) * W * n)))
+        return rc;
+    hipLaunchKernelGGL(split_draws_kernel, dim3((unsigned)n_steps), dim3(kSplitThreads), 0, st, t.block, t.keys, t.sets,
+                       H, D, seed, step0, a, (flags & RVK_STRETCH_FIXED_SPLIT) ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    t.H = H;
+    t.steps = n_steps;
     return RVK_OK;
 }
 
@@ -344,19 +389,20 @@ int rvk_logpost(rvk_post *p, const double *xf, int64_t W, int64_t stride, double
 }
 
 int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n_steps, double a, uint64_t seed,
-                    uint64_t step0, const int32_t *d_set, const double *d_zu, const int32_t *d_rint,
+                    uint64_t step0, int32_t flags, const int32_t *d_set, const double *d_zu, const int32_t *d_rint,
                     const double *d_au, double *d_chain, double *d_lnp, int64_t *d_naccepted, int32_t *d_status,
                     void *stream) {
     if (!p) return fail(RVK_E_ARG, "NULL posterior");
     if (W < 4 || (W & 1)) return fail(RVK_E_ARG, "n_walkers must be even and >= 4");
     if (n_steps < 0) return fail(RVK_E_ARG, "n_steps < 0");
     if (!(a > 1.0)) return fail(RVK_E_ARG, "stretch scale a must be > 1");
+    if (flags & ~RVK_STRETCH_FIXED_SPLIT) return fail(RVK_E_ARG, "unknown flags");
     if (!d_x || !d_lp || !d_status) return fail(RVK_E_ARG, "NULL device buffer");
     if (d_set && (!d_zu || !d_rint || !d_au)) return fail(RVK_E_ARG, "host draws need set, zu, rint and au");
     if (n_steps == 0) return RVK_OK;
     const long long H = W / 2;
     int rc = reserve_impl(p, H);
-    if (rc) return rc;
+    if (rc || (rc = reserve_chunk(p, H))) return rc;
     rvk_handle *h = p->h;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
@@ -364,58 +410,117 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
     HIPCHK(hipStreamIsCapturing(st, &cs));
     const bool use_graph = h->graph && cs == hipStreamCaptureStatusNone;   // a caller's capture records the launches
     const size_t wd = (size_t)W * (size_t)p->n_free, hh = 2 * (size_t)H;
-    for (int s0 = 0; s0 < n_steps; s0 += kStepsPerGraph) {
-        const int n = (n_steps - s0) < kStepsPerGraph ? (n_steps - s0) : kStepsPerGraph;
-        RunArgs run{d_x,
-                    d_lp,
-                    (long long *)d_naccepted,
-                    (int *)d_status,
-                    d_chain ? d_chain + (size_t)s0 * wd : nullptr,
-                    d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
-                    d_set ? d_set + (size_t)s0 * hh : nullptr,
-                    d_set ? d_zu + (size_t)s0 * hh : nullptr,
-                    d_set ? d_rint + (size_t)s0 * hh : nullptr,
-                    d_set ? d_au + (size_t)s0 * hh : nullptr,
-                    seed,
-                    step0 + (uint64_t)s0,
-                    a};
-        if (uses_pre(p)) {
+    const int blk = d_set ? n_steps : draws_block_steps(H);               // steps per device draw block
+    for (int b0 = 0; b0 < n_steps; b0 += blk) {
+        const int nb = (n_steps - b0) < blk ? (n_steps - b0) : blk;
+        if (!d_set && (rc = draws_fill(p->tab, st, H, nb, p->n_free, seed, step0 + (uint64_t)b0, a, flags))) return rc;
+        for (int s0 = b0; s0 < b0 + nb; s0 += kStepsPerGraph) {
+            const int n = (b0 + nb - s0) < kStepsPerGraph ? (b0 + nb - s0) : kStepsPerGraph;
+            RunArgs run{d_x,
+                        d_lp,
+                        (long long *)d_naccepted,
+                        (int *)d_status,
+                        d_chain ? d_chain + (size_t)s0 * wd : nullptr,
+                        d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
+                        d_set ? d_set + (size_t)s0 * hh : nullptr,
+                        d_set ? d_zu + (size_t)s0 * hh : nullptr,
+                        d_set ? d_rint + (size_t)s0 * hh : nullptr,
+                        d_set ? d_au + (size_t)s0 * hh : nullptr,
+                        seed,
+                        step0 + (uint64_t)s0,
+                        a};
             const long long np = (long long)n * 2 * H;
-            hipLaunchKernelGGL(set_run_draws_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, p->d_run,
-                               run, p->d_pre, n, H, p->n_free);
-        } else {
-            hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
-        }
-        if (use_graph && n == kStepsPerGraph) {
-            if ((rc = ensure_graph(p, H))) return rc;
-            HIPCHK(hipGraphLaunch(p->graph, st));
-        } else {
-            enqueue_steps(p, st, H, n);
+            hipLaunchKernelGGL(chunk_args_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, p->d_run, run,
+                               p->d_pre, d_set ? nullptr : p->tab.block + (size_t)(s0 - b0) * hh, n, H, p->n_free);
+            if (use_graph && n == kStepsPerGraph) {
+                if ((rc = ensure_graph(p, H))) return rc;
+                HIPCHK(hipGraphLaunch(p->graph, st));
+            } else {
+                enqueue_steps(p, st, H, n);
+            }
         }
     }
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }
 
-int rvk_stretch_half(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t half, int64_t j0, int64_t count,
-                     double a, uint64_t seed, uint64_t step, int64_t *d_naccepted, int32_t *d_status, void *stream) {
+int rvk_stretch_draws(rvk_post *p, int64_t W, int32_t n_steps, double a, uint64_t seed, uint64_t step0, int32_t flags,
+                      void *stream) {
     if (!p) return fail(RVK_E_ARG, "NULL posterior");
     if (W < 4 || (W & 1)) return fail(RVK_E_ARG, "n_walkers must be even and >= 4");
-    if (half != 0 && half != 1) return fail(RVK_E_ARG, "half must be 0 or 1");
-    const long long H = W / 2;
-    if (j0 < 0 || count < 0 || j0 + count > H) return fail(RVK_E_ARG, "proposal slice outside the half");
+    if (n_steps < 1) return fail(RVK_E_ARG, "n_steps must be >= 1");
     if (!(a > 1.0)) return fail(RVK_E_ARG, "stretch scale a must be > 1");
-    if (!d_x || !d_lp || !d_status) return fail(RVK_E_ARG, "NULL device buffer");
+    if (flags & ~RVK_STRETCH_FIXED_SPLIT) return fail(RVK_E_ARG, "unknown flags");
+    HIPCHK(hipSetDevice(p->h->device));
+    return draws_fill(p->tab, (hipStream_t)stream, W / 2, n_steps, p->n_free, seed, step0, a, flags);
+}
+
+int rvk_stretch_propose(rvk_post *p, const double *d_x, int64_t W, int32_t s, int32_t half, int64_t j0, int64_t count,
+                        double *d_out, void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL posterior");
+    const long long H = W / 2;
+    if (W < 4 || (W & 1) || H != p->tab.H) return fail(RVK_E_ARG, "n_walkers differs from the drawn table's");
+    if (s < 0 || s >= p->tab.steps) return fail(RVK_E_ARG, "step outside the drawn table");
+    if (half != 0 && half != 1) return fail(RVK_E_ARG, "half must be 0 or 1");
+    if (j0 < 0 || count < 0 || j0 + count > H) return fail(RVK_E_ARG, "proposal slice outside the half");
+    if (!d_x || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     if (count == 0) return RVK_OK;
     int rc = reserve_impl(p, count);
     if (rc) return rc;
     rvk_handle *h = p->h;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
-    const RunArgs run{d_x, d_lp, (long long *)d_naccepted, (int *)d_status, nullptr, nullptr,
-                      nullptr, nullptr, nullptr, nullptr, seed, step, a};
+    const RunArgs run{const_cast<double *>(d_x), nullptr, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, nullptr, 0, 0, 2.0};
     hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
-    enqueue_half(p, st, 0, half, j0, count, H, nullptr);
+    const PostDev pd = p->dev();
+    const PostArgs post{p->d_lp, p->jac, p->renorm};
+    if (p->fusable && h->solver == 0 && h->sample_eval[p->ext]) {
+        const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, H, p->tab.block,
+                            d_out};
+        h->sample_eval[p->ext](st, h->epochs(), h->n, h->n_inst, nullptr, count, h->p_full(), post, sa);
+    } else {
+        hipLaunchKernelGGL(propose_kernel, dim3(wave_blocks(count)), dim3(256), 0, st, pd, p->d_run, p->tab.block, s,
+                           half, count, j0, H, p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_lau, p->d_sidx);
+        h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, count, h->p_full(), d_out, post);
+    }
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_stretch_table_read(rvk_post *p, int32_t s, int32_t half, int64_t *walker, int64_t *complement, double *z) {
+    if (!p) return fail(RVK_E_ARG, "NULL posterior");
+    if (s < 0 || s >= p->tab.steps || (half != 0 && half != 1)) return fail(RVK_E_ARG, "step / half outside the table");
+    if (!walker || !complement || !z) return fail(RVK_E_ARG, "NULL host buffer");
+    const long long H = p->tab.H;
+    std::vector<PreDraw> v((size_t)H);
+    HIPCHK(hipSetDevice(p->h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(v.data(), p->tab.block + ((size_t)s * 2 + (size_t)half) * (size_t)H, sizeof(PreDraw) * (size_t)H,
+                     hipMemcpyDeviceToHost));
+    for (long long j = 0; j < H; ++j) {
+        walker[j] = v[(size_t)j].s;
+        complement[j] = v[(size_t)j].c;
+        z[j] = v[(size_t)j].z;
+    }
+    return RVK_OK;
+}
+
+int rvk_stretch_update(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t s, int32_t half,
+                       const double *d_nlp, double *d_chain_step, double *d_lnp_step, const int64_t *d_nacc_in,
+                       int64_t *d_nacc_out, int32_t *d_status, void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL posterior");
+    const long long H = W / 2;
+    if (W < 4 || (W & 1) || H != p->tab.H) return fail(RVK_E_ARG, "n_walkers differs from the drawn table's");
+    if (s < 0 || s >= p->tab.steps) return fail(RVK_E_ARG, "step outside the drawn table");
+    if (half != 0 && half != 1) return fail(RVK_E_ARG, "half must be 0 or 1");
+    if (!d_x || !d_lp || !d_nlp || !d_status) return fail(RVK_E_ARG, "NULL device buffer");
+    if (d_nacc_out && !d_nacc_in) return fail(RVK_E_ARG, "d_nacc_out needs d_nacc_in");
+    HIPCHK(hipSetDevice(p->h->device));
+    hipLaunchKernelGGL(stretch_update_kernel, dim3(blocks_for(H)), dim3(256), 0, (hipStream_t)stream,
+                       p->tab.block + ((size_t)s * 2 + (size_t)half) * (size_t)H, H, p->n_free, d_x, d_lp, d_nlp,
+                       (const long long *)d_nacc_in, (long long *)d_nacc_out, (int *)d_status, d_chain_step,
+                       d_lnp_step);
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

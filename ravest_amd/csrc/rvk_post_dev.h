@@ -67,11 +67,10 @@ __device__ __forceinline__ double prior_lp_basic(int kind, const double *p, doub
     }
 }
 
-// One prior term, the reference's formula and bounds (prior.py).
-inline __device__ double prior_lp(const PriorSlot &s, double x) {
-    const double *p = s.p;
-    if (s.kind <= kMaxBasicPriorKind) return prior_lp_basic(s.kind, p, x);
-    switch (s.kind) {
+// The prior kinds with a transcendental function (Rayleigh, VanEylen19Mixture, Beta), out of
+// line: their log / log1p / exp cost registers only while they run.
+__device__ __attribute__((noinline)) double prior_lp_trans(int kind, const double *p, double x) {
+    switch (kind) {
         case RVK_PRIOR_RAYLEIGH:
             if (x < 0.0) return -INFINITY;
             return rayleigh_lp(x, p[0], p[1]);
@@ -101,6 +100,12 @@ inline __device__ double prior_lp(const PriorSlot &s, double x) {
     }
 }
 
+// One prior term, the reference's formula and bounds (prior.py).
+inline __device__ double prior_lp(const PriorSlot &s, double x) {
+    if (s.kind <= kMaxBasicPriorKind) return prior_lp_basic(s.kind, s.p, x);
+    return prior_lp_trans(s.kind, s.p, x);
+}
+
 // ---- Philox4x32-10 (counter-based; Salmon et al. 2011) -------------------------------
 __device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
 #pragma unroll
@@ -118,15 +123,9 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 
-// Draws of one (step, half, walker-in-half).
-struct Draw {
-    long long s, c;     // active walker, complementary walker
-    double zu, au;
-};
-
-// Per-call arguments of rvk_stretch_run, kept in device memory (written by a one-thread
-// kernel at the start of each chunk of steps) so that the kernels of a chunk have
-// call-invariant arguments and can be replayed from a cached HIP graph.
+// Per-call arguments of rvk_stretch_run, kept in device memory (written by a small kernel at
+// the start of each chunk of steps) so that the kernels of a chunk have call-invariant
+// arguments and can be replayed from a cached HIP graph.
 struct RunArgs {
     double *x;            // [W][D] walker state (in/out)
     double *lp;           // [W]
@@ -142,47 +141,173 @@ struct RunArgs {
     double a;
 };
 
-__device__ __forceinline__ Draw draw(const RunArgs &r, int step, int half, long long j, long long H) {
-    Draw d;
-    if (r.set) {
-        const long long o = ((long long)step * 2 + half) * H + j;
-        const long long ob = ((long long)step * 2 + (1 - half)) * H;
-        d.s = r.set[o];
-        d.c = r.set[ob + r.rint[o]];
-        d.zu = r.zu[o];
-        d.au = r.au[o];
-    } else {
-        const uint64_t st = r.step0 + (uint64_t)step;
-        const uint2 key = make_uint2((uint32_t)r.seed, (uint32_t)(r.seed >> 32));
-        const uint4 a = philox(make_uint4((uint32_t)j, (uint32_t)half, (uint32_t)st, (uint32_t)(st >> 32)), key);
-        const uint4 b = philox(make_uint4((uint32_t)j, (uint32_t)half | 2u, (uint32_t)st, (uint32_t)(st >> 32)), key);
-        d.s = (long long)half * H + j;
-        // complement index in [0, H): multiply-shift (bias <= H / 2^32)
-        d.c = (long long)(1 - half) * H + (long long)(((uint64_t)b.x * (uint64_t)H) >> 32);
-        d.zu = u53(a.x, a.y);
-        d.au = u53(a.z, a.w);
-    }
-    return d;
-}
-
-// One proposal's draws as the fused half-step uses them, precomputed for a chunk of steps by
-// set_run_draws_kernel: the walker and its complement, z, (D - 1) log z and log u'.  The same
-// expressions as the fused kernel's in-kernel path (make_pre), so either gives the same bits.
+// One proposal's draws, as every sampler kernel consumes them: the walker and its complement,
+// z, (D - 1) log z and log u'.  Made by split_draws_kernel (device Philox) or from host draws
+// (emcee's RandomState stream) by chunk_args_kernel -- the same expressions either way.
 struct PreDraw {
     double z, fac, lau;
     long long s, c;
 };
 
-__device__ __forceinline__ PreDraw make_pre(const RunArgs &r, int step, int half, long long j, long long H, int D) {
-    const Draw dr = draw(r, step, half, j, H);
-    const double zt = (r.a - 1.0) * dr.zu + 1.0;
+// StretchMove.get_proposal: z = ((a - 1) u + 1)^2 / a (emcee 3.1, moves/stretch.py)
+__device__ __forceinline__ PreDraw pre_from(double zu, double au, long long s, long long c, double a, int D) {
+    const double zt = (a - 1.0) * zu + 1.0;
     PreDraw p;
-    p.z = zt * zt / r.a;
+    p.z = zt * zt / a;
     p.fac = ((double)D - 1.0) * log(p.z);
-    p.lau = log(dr.au);
-    p.s = dr.s;
-    p.c = dr.c;
+    p.lau = log(au);
+    p.s = s;
+    p.c = c;
     return p;
+}
+
+// q = c - (c - s) z as one fused multiply-add (every sampler path: the proposal has the same
+// bits wherever it is formed -- the fused half-step, propose_kernel, the sharded update).
+__device__ __forceinline__ double stretch_q(double xc, double xs, double z) { return __builtin_fma(xs - xc, z, xc); }
+
+// RedBlueMove.propose: accept when (ndim - 1) log z + lp(q) - lp(s) > log u'
+__device__ __forceinline__ bool stretch_accept(double fac, double nlp, double lp_old, double lau) {
+    return fac + nlp - lp_old > lau;
+}
+
+// Host-supplied draws (emcee's call order, sampler.emcee_step_draws) of (step, half, j).
+__device__ __forceinline__ PreDraw make_pre_host(const RunArgs &r, int step, int half, long long j, long long H,
+                                                 int D) {
+    const long long o = ((long long)step * 2 + half) * H + j;
+    const long long ob = ((long long)step * 2 + (1 - half)) * H;
+    return pre_from(r.zu[o], r.au[o], r.set[o], r.set[ob + r.rint[o]], r.a, D);
+}
+
+// Flags of the device draws (include/rvk_post.h RVK_STRETCH_*).
+constexpr int kSplitThreads = 1024;
+
+// Block-wide exclusive prefix sum of one int per thread (blockDim.x <= 1024); `total` gets the sum.
+__device__ __forceinline__ long long block_excl_scan(long long v, long long *wtot, long long &total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    long long x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wtot[wv] = x;
+    __syncthreads();
+    long long before = 0;
+    total = 0;
+    for (int k = 0; k < nw; ++k) {
+        const long long w = wtot[k];
+        if (k < wv) before += w;
+        total += w;
+    }
+    __syncthreads();   // wtot is reused by the next scan
+    return before + x - v;
+}
+
+// Every draw of n steps of the stretch move, one workgroup of kSplitThreads per step (grid n):
+//   * the split (emcee 3.1 RedBlueMove, randomize_split=True: inds = arange(W) % 2 shuffled,
+//     half h = the walkers with inds == h, ascending): each walker gets a 32-bit Philox key and
+//     half 0 is the H walkers with the smallest (key, index) -- a uniformly random balanced
+//     split, found by an 8-bit radix select of the H-th smallest key and two block scans; with
+//     RVK_STRETCH_FIXED_SPLIT the halves are the even / odd walkers (randomize_split=False);
+//   * per proposal j of each half: u (for z), u' (acceptance) and the complement index
+//     r in [0, H) (multiply-shift, bias <= H / 2^32), keyed by (j, half, global step) -- so a
+//     draw does not depend on how proposals are shared out between launches or GPUs.
+// table[s][half][j] = PreDraw; keys / sets are scratch [n][W].
+static __global__ __launch_bounds__(kSplitThreads) void split_draws_kernel(PreDraw *__restrict__ table,
+                                                                           uint32_t *__restrict__ keys_g,
+                                                                           int32_t *__restrict__ sets_g, long long H,
+                                                                           int D, uint64_t seed, uint64_t step0,
+                                                                           double a, int fixed) {
+    __shared__ int hist[256];
+    __shared__ long long wtot[kSplitThreads / 64];
+    __shared__ unsigned sh_prefix;
+    __shared__ long long sh_k;
+    const int s = blockIdx.x;
+    const uint64_t st = step0 + (uint64_t)s;
+    const long long W = 2 * H;
+    const int t = threadIdx.x, nt = blockDim.x;
+    const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+    int32_t *set = sets_g + (size_t)s * (size_t)W;                      // [0, H): half 0, [H, 2H): half 1
+    if (fixed) {
+        for (long long i = t; i < W; i += nt) set[(i & 1) * H + (i >> 1)] = (int32_t)i;
+    } else {
+        uint32_t *kk = keys_g + (size_t)s * (size_t)W;
+        const long long C = (W + nt - 1) / nt;                           // contiguous walkers per thread
+        const long long i0 = (long long)t * C, i1 = (i0 + C < W) ? i0 + C : W;
+        for (long long i = i0; i < i1; ++i)
+            kk[i] = philox(make_uint4((uint32_t)i, 4u, (uint32_t)st, (uint32_t)(st >> 32)), key).x;
+        unsigned prefix = 0, pmask = 0;
+        long long k = H;                                                 // rank (1-based) of the threshold
+        for (int pass = 0; pass < 4; ++pass) {
+            const int shift = 24 - 8 * pass;
+            for (int b = t; b < 256; b += nt) hist[b] = 0;
+            __syncthreads();
+            for (long long i = i0; i < i1; ++i) {
+                const uint32_t u = kk[i];
+                if ((u & pmask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1);
+            }
+            __syncthreads();
+            if (t < 64) {                                                // lane l: bins 4l .. 4l + 3
+                const int c0 = hist[4 * t], c1 = hist[4 * t + 1], c2 = hist[4 * t + 2], c3 = hist[4 * t + 3];
+                long long x = (long long)c0 + c1 + c2 + c3;
+                const long long own = x;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const long long y = __shfl_up(x, d, 64);
+                    if (t >= d) x += y;
+                }
+                long long ex = x - own;                                  // keys in bins below 4l
+                if (ex < k && k <= x) {                                  // exactly one lane
+                    int dig = 4 * t;
+                    const int cs[4] = {c0, c1, c2, c3};
+                    for (int q = 0; q < 4; ++q) {
+                        if (k <= ex + cs[q]) {
+                            dig = 4 * t + q;
+                            break;
+                        }
+                        ex += cs[q];
+                    }
+                    sh_prefix = prefix | ((unsigned)dig << shift);
+                    sh_k = k - ex;
+                }
+            }
+            __syncthreads();
+            prefix = sh_prefix;
+            k = sh_k;
+            pmask |= 255u << shift;
+            __syncthreads();
+        }
+        // half 0 = keys < T, plus the first k (by index) of the keys == T
+        const uint32_t T = prefix;
+        long long neq = 0;
+        for (long long i = i0; i < i1; ++i) neq += kk[i] == T;
+        long long tot;
+        const long long eq0 = block_excl_scan(neq, wtot, tot);
+        long long nin = 0, r = eq0;
+        for (long long i = i0; i < i1; ++i) {
+            const uint32_t u = kk[i];
+            if (u < T) ++nin;
+            else if (u == T) nin += (r++ < k);
+        }
+        long long m = block_excl_scan(nin, wtot, tot);                  // walkers of half 0 before i0
+        r = eq0;
+        for (long long i = i0; i < i1; ++i) {
+            const uint32_t u = kk[i];
+            const bool in0 = u < T || (u == T && r++ < k);
+            if (in0) set[m++] = (int32_t)i;
+            else set[H + (i - m)] = (int32_t)i;                          // i - m = half-1 walkers before i
+        }
+    }
+    __syncthreads();                                                     // the block's set writes
+    for (long long q = t; q < W; q += nt) {
+        const int half = q >= H;
+        const long long j = q - (half ? H : 0);
+        const uint4 ra = philox(make_uint4((uint32_t)j, (uint32_t)half, (uint32_t)st, (uint32_t)(st >> 32)), key);
+        const uint4 rb = philox(make_uint4((uint32_t)j, (uint32_t)half | 2u, (uint32_t)st, (uint32_t)(st >> 32)), key);
+        const long long rr = (long long)(((uint64_t)rb.x * (uint64_t)H) >> 32);
+        table[((long long)s * 2 + half) * H + j] =
+            pre_from(u53(ra.x, ra.y), u53(ra.z, ra.w), set[half * H + j], set[(1 - half) * H + rr], a, D);
+    }
 }
 
 // Per-walker prologue, one wave per walker: x (n_free coordinates, in LDS `lx`)
@@ -281,29 +406,36 @@ struct SampleArgs {
     int D;                      // n_free
     const double *q;            // [H][D] proposals
     const double *fac;          // [H] (ndim - 1) log z
-    const double *au;           // [H] acceptance uniforms
+    const double *lau;          // [H] log of the acceptance uniforms
     const long long *sidx;      // [H] walker index of proposal w
     const RunArgs *run;         // state, chain and status pointers
     int step;                   // step within the chunk
-    int half;                   // active half (fused proposals, SAMPLE == 2)
-    PostDev pd;                 // the posterior (fused proposals, SAMPLE == 2)
+    int half;                   // active half (fused proposals, SAMPLE >= 2)
+    PostDev pd;                 // the posterior (fused proposals, SAMPLE >= 2)
     long long j0;               // the launch's proposals are j0 .. j0 + count - 1 of the half
     long long hfull;            // walkers per half (the complement's range; chain row stride / 2)
-    const PreDraw *pre;         // [steps][2][hfull] this chunk's draws, or nullptr (drawn in the kernel)
+    const PreDraw *pre;         // [steps][2][hfull] the draws, indexed by (step, half, j0 + w)
+    double *out;                // SAMPLE == 3: out[w] = the proposal's log-posterior (no accept / reject)
 };
 
-// Limits of the fused proposal path (loglike_kernel SAMPLE == 2): the proposal, its full row
-// and the old state are staged in LDS per walker of a pass; priors basic kinds only, no
-// prior-side conversion.
-constexpr int kFuseMaxD = 16;
-constexpr int kFuseMaxPFull = 32;
-constexpr int kFuseMaxPrior = 32;
+// Limits of the fused proposal path (loglike_kernel SAMPLE >= 2): lane c of the walker's wave
+// holds coordinate c, column c of the full row and prior slot c, so each is at most a wave;
+// every built-in prior kind and the prior-side conversion (Case 3) are evaluated in the prep.
+constexpr int kFuseMaxD = 64;
+constexpr int kFuseMaxPFull = 64;
+constexpr int kFuseMaxPrior = 64;
+
+// Out of line (atan/tan/atan2 for the Tc and secosw/sesinw forms): the prior-side conversion
+// of one planet (fit.py:3418-3446) costs registers only while it runs.
+__device__ __attribute__((noinline)) bool to_default_call(int par, const double *p5, double *d5) {
+    return to_default_t<-1>(p5, d5[0], d5[1], d5[2], d5[3], d5[4], par);
+}
 
 // Accept / reject (RedBlueMove.propose + update) and the chain write of the half, for the
 // unfused path (reference solver) and the GP sampler: one thread per proposal.
 static __global__ __launch_bounds__(256) void stretch_accept_kernel(const RunArgs *__restrict__ runp, int step, long long H, int D,
                                                      const double *__restrict__ q, const double *__restrict__ fac,
-                                                     const double *__restrict__ au,
+                                                     const double *__restrict__ lau,
                                                      const long long *__restrict__ sidx,
                                                      const double *__restrict__ nlp_all) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -312,9 +444,8 @@ static __global__ __launch_bounds__(256) void stretch_accept_kernel(const RunArg
     const long long s = sidx[j];
     const double nlp = nlp_all[j];
     if (isnan(nlp)) atomicOr(run.status, 1);
-    const double lnpdiff = fac[j] + nlp - run.lp[s];
     double *xs = run.x + s * D;
-    if (lnpdiff > log(au[j])) {
+    if (stretch_accept(fac[j], nlp, run.lp[s], lau[j])) {
         for (int k = 0; k < D; ++k) xs[k] = q[j * D + k];
         run.lp[s] = nlp;
         if (run.nacc) run.nacc[s] += 1;
@@ -324,18 +455,51 @@ static __global__ __launch_bounds__(256) void stretch_accept_kernel(const RunArg
     if (run.lnpc) run.lnpc[(long long)step * 2 * H + s] = run.lp[s];
 }
 
+// The multi-GPU half-step's second part (rvk_stretch_update): every rank holds the log-posteriors
+// of ALL H proposals of the half (all-gathered) and applies the accept / reject to the whole half
+// itself, re-forming each proposal from the draws and the (replicated) state exactly as the
+// fused half-step forms it.  One thread per proposal.
+static __global__ __launch_bounds__(256) void stretch_update_kernel(const PreDraw *__restrict__ pre, long long H, int D,
+                                                                    double *__restrict__ x, double *__restrict__ lp,
+                                                                    const double *__restrict__ nlp_all,
+                                                                    const long long *nacc_in, long long *nacc_out,
+                                                                    int *__restrict__ status, double *__restrict__ chain,
+                                                                    double *__restrict__ lnpc) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= H) return;
+    const PreDraw p = pre[j];
+    const double nlp = nlp_all[j];
+    if (isnan(nlp)) atomicOr(status, 1);
+    double *xs = x + p.s * D;
+    const double *xc = x + p.c * D;
+    const bool acc = stretch_accept(p.fac, nlp, lp[p.s], p.lau);
+    for (int k = 0; k < D; ++k) {
+        const double v = acc ? stretch_q(xc[k], xs[k], p.z) : xs[k];
+        if (acc) xs[k] = v;
+        if (chain) chain[p.s * D + k] = v;
+    }
+    if (acc) lp[p.s] = nlp;
+    if (nacc_out) nacc_out[p.s] = nacc_in[p.s] + (acc ? 1 : 0);   // in == out: a running count
+    if (lnpc) lnpc[p.s] = lp[p.s];
+}
+
 static __global__ void set_run_kernel(RunArgs *dst, RunArgs v) { *dst = v; }
 
-// The chunk's arguments plus, for the fused half-step, every proposal's draws of its n steps
-// (one thread per proposal): the fused kernel then reads one PreDraw (a wave-uniform address)
-// instead of running two Philox blocks on its critical path.
-static __global__ __launch_bounds__(256) void set_run_draws_kernel(RunArgs *dst, RunArgs v, PreDraw *pre, int n,
-                                                                   long long H, int D) {
+// The chunk's arguments plus every proposal's draws of its n steps (one thread per proposal) at
+// the chunk's fixed address `pre` (so a cached graph of the chunk reads them): a copy of the
+// device draws (`src`, split_draws_kernel) or, with host draws (v.set), the PreDraw of each.
+static __global__ __launch_bounds__(256) void chunk_args_kernel(RunArgs *dst, RunArgs v, PreDraw *__restrict__ pre,
+                                                                const PreDraw *__restrict__ src, int n, long long H,
+                                                                int D) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *dst = v;
     if (i >= (long long)n * 2 * H) return;
-    const long long sh = i / H;
-    pre[i] = make_pre(v, (int)(sh >> 1), (int)(sh & 1), i - sh * H, H, D);
+    if (src) {
+        pre[i] = src[i];
+    } else {
+        const long long sh = i / H;
+        pre[i] = make_pre_host(v, (int)(sh >> 1), (int)(sh & 1), i - sh * H, H, D);
+    }
 }
 
 

@@ -134,29 +134,81 @@ class ShardedDevicePosterior:
         return out
 
 
-class ShardedDeviceSampler:
-    """The device stretch move over several GPUs (one process per GPU): config 4's 65536 walkers
-    as a sampler, not only as a batch evaluator (SURVEY.md §8(e) + §8(f) row 3).
+class LibStretchOps:
+    """The device stretch move's operations for ShardedDeviceSampler, on librvk
+    (include/rvk_post.h): draws, slice evaluation, whole-half update."""
 
-    Every rank holds the whole walker state x [W, D], lp [W] in its HBM.  Per half-step each rank
-    makes, evaluates and accepts/rejects its contiguous slice of the active half's proposals
-    (rvk_stretch_half: Philox draws keyed by the global proposal index and step, so the union
-    over ranks is exactly the single-GPU half-step), then the updated rows of the half are
-    all-gathered in place (RCCL over xGMI; x and lp of the half packed in one buffer, one
-    collective per half-step) before the next half-step reads them as its complement.  The chain
-    equals DeviceEnsembleSampler(rng="philox") with the same seed bit for bit at any world size.
-    With the gloo backend (CPU tests, or a 1-GPU rehearsal with several ranks on one device) the
-    gather is staged through host memory.  Replaces ravest's pool.map over walkers
-    (fit.py:1068-1075) for a run that does not fit one GPU's time budget."""
+    def __init__(self, post) -> None:
+        self.post = post
+        self.n_free = post.n_free
 
-    def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed: int = 0, group=None) -> None:
+    def reserve(self, n: int) -> None:
+        self.post.reserve(n)
+
+    def logpost(self, x, out, stream) -> None:
+        self.post.device(x, out, stream)
+
+    def draws(self, W, n, a, seed, step0, flags, stream) -> None:
+        from . import _lib
+        _lib.check(_lib.load().rvk_stretch_draws(self.post._p, W, n, a, seed, step0, flags, stream.cuda_stream))
+
+    def propose(self, x, W, s, half, j0, count, out, stream) -> None:
+        from . import _lib
+        _lib.check(_lib.load().rvk_stretch_propose(self.post._p, x.data_ptr(), W, s, half, j0, count, out.data_ptr(),
+                                                   stream.cuda_stream))
+
+    def update(self, x, lp, W, s, half, nlp, chain_step, lnp_step, nacc_in, nacc_out, status, stream) -> None:
+        from . import _lib
+        _lib.check(_lib.load().rvk_stretch_update(self.post._p, x.data_ptr(), lp.data_ptr(), W, s, half, nlp.data_ptr(),
+                                                  chain_step.data_ptr(), lnp_step.data_ptr(), nacc_in.data_ptr(),
+                                                  nacc_out.data_ptr(), status.data_ptr(), stream.cuda_stream))
+
+
+from .sampler import _Chunk, _DevicePipeline  # noqa: E402
+
+
+class ShardedDeviceSampler(_DevicePipeline):
+    """The device stretch move over several GPUs, one process per GPU: config 4's 65536 walkers as
+    a sampler (SURVEY.md §8(e) + §8(f) row 3), with emcee 3.1's interface (``sample``,
+    ``run_mcmc``, ``iteration``, ``get_chain``, ``get_autocorr_time``, ...).  Replaces ravest's
+    ``pool.map`` over walkers (fit.py:1068-1075).
+
+    Every rank holds the whole ensemble (x [W, D], lp [W]) and the same Philox draws (keyed by
+    seed, global step and proposal).  Per half-step rank r evaluates only its contiguous slice of
+    the H = W/2 proposals (rvk_stretch_propose), the H per-proposal log-posteriors are
+    all-gathered -- the one exchange, H x 8 bytes in all (RCCL over xGMI with the "nccl"
+    backend; staged through host memory with gloo) -- and every rank applies the accept / reject
+    to the whole half itself (rvk_stretch_update), so the state stays replicated without moving
+    any coordinates.  The chain equals DeviceEnsembleSampler(rng="philox") with the same seed
+    and split bit for bit at any world size; a NaN log-probability is seen by every rank in the
+    gathered block, so all ranks raise together.  (On one GPU DeviceEnsembleSampler is faster:
+    one fused kernel per half-step instead of evaluate + update.)
+
+    ``keep_chain``: "all", or the rank that copies the chain to its host memory (the others
+    keep only the device chunk); ``get_autocorr_time`` is then computed on that rank and
+    broadcast, so call it on every rank, as ravest's convergence loop does."""
+
+    def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed: int = 0, group=None,
+                 randomize_split: bool = True, steps_per_call: int = 256, keep_chain="all",
+                 ops=None, device=None) -> None:
         import torch
         import torch.distributed as dist
-        from .posterior import DevicePosterior
-        self.post = log_posterior if isinstance(log_posterior, DevicePosterior) else DevicePosterior(log_posterior)
-        self.nwalkers, self.ndim, self.a, self.seed = nwalkers, self.post.n_free, float(a), int(seed)
+        if ops is None:
+            from .gp import DeviceGPPosterior, GPLogPosterior
+            from .posterior import DevicePosterior
+            if isinstance(log_posterior, (GPLogPosterior, DeviceGPPosterior)):
+                raise TypeError("ShardedDeviceSampler shards the Keplerian log-posterior (rvk_stretch_propose / "
+                                "rvk_stretch_update); a GP posterior runs on one GPU per chain with "
+                                "DeviceEnsembleSampler")
+            post = log_posterior if isinstance(log_posterior, DevicePosterior) else DevicePosterior(log_posterior)
+            ops = LibStretchOps(post)
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.ops = ops
+        self.nwalkers, self.ndim, self.a, self.seed = nwalkers, ops.n_free, float(a), int(seed)
         if nwalkers % 2 or nwalkers < 4 or nwalkers < 2 * self.ndim:
             raise ValueError("nwalkers must be even, >= 4 and >= 2 * ndim")
+        self.randomize_split = bool(randomize_split)
+        self.steps_per_call = max(1, int(steps_per_call))
         self.group = group
         self.dist = dist
         init = dist.is_available() and dist.is_initialized()
@@ -167,86 +219,115 @@ class ShardedDeviceSampler:
         if H % self.world:
             raise ValueError(f"walkers per half ({H}) must divide evenly over {self.world} ranks")
         self.chunk = H // self.world
-        self.device = torch.device("cuda", torch.cuda.current_device())
-        self.post.reserve(self.chunk)
-        self.iteration = 0
-        self._chain, self._lnp = [], []
-        self.naccepted = np.zeros(nwalkers, dtype=np.int64)
+        if keep_chain != "all" and not (isinstance(keep_chain, int) and 0 <= keep_chain < self.world):
+            raise ValueError("keep_chain must be 'all' or a rank")
+        self.keep_chain = keep_chain
+        ops.reserve(self.chunk)
+        self._pipeline_init(device, keep_host=keep_chain == "all" or keep_chain == self.rank)
+        self._nlp_local = torch.empty(self.chunk, dtype=torch.float64, device=device)
+        self._nlp_all = torch.empty(H, dtype=torch.float64, device=device)
+        self._nacc_steps = [None, None]       # per slot: [steps_per_call, W] acceptance counts after each step
+        self.exchange_bytes_per_half_step = 0
 
-    def _gather_half(self, state, half):
-        """state [W, D + 1] (x | lp); all-gather the active half's rows, chunk per rank."""
-        import torch
-        H = self.nwalkers // 2
-        rows = state[half * H:(half + 1) * H]
-        mine = rows[self.rank * self.chunk:(self.rank + 1) * self.chunk]
-        if self.world == 1:
-            return
-        if self.rccl:
-            self.dist.all_gather_into_tensor(rows.reshape(-1), mine.reshape(-1).clone(), group=self.group)
-        else:
-            out = torch.empty(rows.numel(), dtype=torch.float64)
-            self.dist.all_gather_into_tensor(out, mine.reshape(-1).cpu(), group=self.group)
-            rows.copy_(out.view_as(rows))
-
-    def run_mcmc(self, initial_state, nsteps: int):
-        import torch
+    def _flags(self) -> int:
         from . import _lib
-        W, D = self.nwalkers, self.ndim
-        x0 = np.array(initial_state, dtype=np.float64, copy=True)
-        if x0.shape != (W, D):
-            raise ValueError(f"initial_state must have shape ({W}, {D})")
-        dev = self.device
-        x = torch.from_numpy(x0).to(dev)
-        lp = torch.empty(W, dtype=torch.float64, device=dev)
-        stream = torch.cuda.current_stream(dev)
-        self.post.device(x, lp, stream)                    # every rank: the whole initial block
-        lp0 = lp.cpu().numpy()
-        if np.any(np.isnan(lp0)) or not np.all(np.isfinite(lp0)):
-            raise ValueError("initial state has NaN or -inf log-probabilities")
-        # packed state for the gathers: columns 0..D-1 = x, column D = lp (the kernel reads the views)
-        state = torch.empty((W, D + 1), dtype=torch.float64, device=dev)
-        nacc = torch.zeros(W, dtype=torch.int64, device=dev)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
-        L = _lib.load()
-        H = W // 2
+        return 0 if self.randomize_split else _lib.STRETCH_FIXED_SPLIT
+
+    def _initial_log_prob(self, x, lp) -> None:
+        self.ops.logpost(x, lp, self._stream())
+
+    def _gather(self, stream) -> None:
+        import torch
+        if self.world == 1:
+            self._nlp_all.copy_(self._nlp_local)
+        elif self.rccl:
+            self.dist.all_gather_into_tensor(self._nlp_all, self._nlp_local, group=self.group)
+        else:                                 # gloo: staged through host memory
+            out = torch.empty(self._nlp_all.numel(), dtype=torch.float64)
+            self.dist.all_gather_into_tensor(out, self._nlp_local.cpu(), group=self.group)
+            self._nlp_all.copy_(out)
+        self.exchange_bytes_per_half_step = self._nlp_all.numel() * self._nlp_all.element_size()
+
+    def _begin_chunk(self, ch: _Chunk) -> None:
+        import torch
+        if self._nacc_steps[ch.slot] is None:
+            self._nacc_steps[ch.slot] = torch.empty((self.steps_per_call, self.nwalkers), dtype=torch.int64,
+                                                    device=self.device)
+        ch.x0 = ch.lp0 = ch.nacc0 = ch.draws = ch.rstate0 = None
+
+    def _run_chunk(self, ch: _Chunk, chain_d, lnp_d, stream) -> None:
+        W, n = self.nwalkers, ch.n
+        ns = self._nacc_steps[ch.slot]
+        self.ops.draws(W, n, self.a, self.seed, ch.start, self._flags(), stream)
         j0 = self.rank * self.chunk
-        xs = torch.empty((W, D), dtype=torch.float64, device=dev)
-        lps = torch.empty(W, dtype=torch.float64, device=dev)
-        xs.copy_(x)
-        lps.copy_(lp)
-        chain = torch.empty((nsteps, W, D), dtype=torch.float64, device=dev)
-        lnpc = torch.empty((nsteps, W), dtype=torch.float64, device=dev)
-        for t in range(nsteps):
+        prev = self._nacc
+        for s in range(n):
             for half in (0, 1):
-                _lib.check(L.rvk_stretch_half(self.post._p, xs.data_ptr(), lps.data_ptr(), W, half, j0, self.chunk,
-                                              self.a, self.seed, self.iteration + t, nacc.data_ptr(),
-                                              status.data_ptr(), stream.cuda_stream))
-                if self.world > 1:
-                    rows = slice(half * H, (half + 1) * H)
-                    state[rows, :D] = xs[rows]
-                    state[rows, D] = lps[rows]
-                    self._gather_half(state, half)
-                    xs[rows] = state[rows, :D]
-                    lps[rows] = state[rows, D]
-            chain[t] = xs
-            lnpc[t] = lps
-        if int(status.item()):
-            raise ValueError("The log_prob was NaN")
-        if self.world > 1:                                 # each rank counted its slices' acceptances
-            if self.rccl:
-                self.dist.all_reduce(nacc, group=self.group)
-            else:
-                c = nacc.cpu()
-                self.dist.all_reduce(c, group=self.group)
-                nacc.copy_(c)
-        self._chain.append(chain.cpu().numpy())
-        self._lnp.append(lnpc.cpu().numpy())
-        self.naccepted += nacc.cpu().numpy()
-        self.iteration += nsteps
-        return xs.cpu().numpy(), lps.cpu().numpy()
+                self.ops.propose(self._x, W, s, half, j0, self.chunk, self._nlp_local, stream)
+                self._gather(stream)
+                self.ops.update(self._x, self._lp, W, s, half, self._nlp_all, chain_d[s], lnp_d[s], prev, ns[s],
+                                self._status, stream)
+            prev = ns[s]
+        self._nacc.copy_(ns[n - 1])
 
-    def get_chain(self) -> np.ndarray:
-        return np.concatenate(self._chain) if self._chain else np.zeros((0, self.nwalkers, self.ndim))
+    def _state_at(self, target: int):
+        """(x, lp, nacc) device views of the state after step `target` (a step of the last chunks,
+        or the initial state): the chunk's own chain rows -- no replay, no collective."""
+        if target == self._x_init[0]:
+            return self._x_init[1], self._x_init[2], self._x_init[3]
+        ch = next((c for c in self._chunks if c.start < target <= c.start + c.n), None)
+        if ch is None:
+            raise RuntimeError("internal: no chunk record covers the requested step")
+        chain_d, lnp_d = self._dbuf[ch.slot]
+        k = target - 1 - ch.start
+        return chain_d[k], lnp_d[k], self._nacc_steps[ch.slot][k]
 
-    def get_log_prob(self) -> np.ndarray:
-        return np.concatenate(self._lnp) if self._lnp else np.zeros((0, self.nwalkers))
+    def _settle(self) -> None:
+        if self._x is None or self._dev_iter == self.iteration:
+            return
+        x, lp, nacc = self._state_at(self.iteration)
+        self._x.copy_(x)
+        self._lp.copy_(lp)
+        self._nacc.copy_(nacc)
+        self._dev_iter = self.iteration
+        self._chunks = []
+        self._x_init = (self._dev_iter, self._x.clone(), self._lp.clone(), self._nacc.clone())
+        self.backend.accepted = self._nacc.cpu().numpy()
+        self._accepted_iter = self.iteration
+
+    @property
+    def naccepted(self):
+        if self._accepted_iter != self.iteration:
+            src = self._nacc if self._dev_iter == self.iteration else self._state_at(self.iteration)[2]
+            self.backend.accepted = src.cpu().numpy()
+            self._accepted_iter = self.iteration
+        return self.backend.accepted
+
+    def get_chain(self, flat=False, thin=1, discard=0):
+        if not self._keep_host:
+            raise RuntimeError(f"rank {self.rank} keeps no chain (keep_chain={self.keep_chain})")
+        return super().get_chain(flat=flat, thin=thin, discard=discard)
+
+    def get_log_prob(self, flat=False, thin=1, discard=0):
+        if not self._keep_host:
+            raise RuntimeError(f"rank {self.rank} keeps no chain (keep_chain={self.keep_chain})")
+        return super().get_log_prob(flat=flat, thin=thin, discard=discard)
+
+    def get_autocorr_time(self, discard=0, thin=1, **kwargs):
+        """emcee's estimate; with keep_chain = r computed on rank r and broadcast (collective)."""
+        import torch
+        if self.keep_chain == "all" or self.world == 1:
+            return super().get_autocorr_time(discard=discard, thin=thin, **kwargs)
+        tau = torch.zeros(self.ndim, dtype=torch.float64, device=self.device if self.rccl else "cpu")
+        err = torch.zeros(1, dtype=torch.float64, device=tau.device)
+        if self.rank == self.keep_chain:
+            try:
+                tau.copy_(torch.from_numpy(super().get_autocorr_time(discard=discard, thin=thin, **kwargs)))
+            except Exception:
+                err.fill_(1.0)
+        self.dist.broadcast(err, self.keep_chain, group=self.group)
+        self.dist.broadcast(tau, self.keep_chain, group=self.group)
+        if float(err[0]):
+            from .sampler import AutocorrError
+            raise AutocorrError(tau.cpu().numpy(), f"autocorrelation estimate failed on rank {self.keep_chain}")
+        return tau.cpu().numpy()

@@ -1,12 +1,14 @@
-"""Affine-invariant ensemble samplers with emcee's StretchMove semantics.
+"""Affine-invariant ensemble samplers with emcee 3.1's EnsembleSampler interface.
 
-ravest's Fitter.run_mcmc drives ``emcee.EnsembleSampler`` (fit.py:1068-1111)
-with the default move, ``StretchMove(a=2)`` = ``RedBlueMove(nsplits=2,
-randomize_split=True)``: each step shuffles ``arange(W) % 2`` into two halves
-and updates each half against the other (proposal ``c - (c - s) z``,
-``z = ((a-1) u + 1)^2 / a``, acceptance ``(ndim-1) log z + lp(q) - lp(s) >
-log u'``).  emcee is not installed in this image, so two samplers provide that
-move here, with emcee's chain layout (steps, walkers, ndim) and accessors:
+ravest's Fitter.run_mcmc / GPFitter.run_mcmc drive ``emcee.EnsembleSampler``
+(fit.py:1068-1160, 4982-5075) with the default move, ``StretchMove(a=2)`` =
+``RedBlueMove(nsplits=2, randomize_split=True)``: each step shuffles
+``arange(W) % 2`` into two halves and updates each half against the other
+(proposal ``c - (c - s) z``, ``z = ((a-1) u + 1)^2 / a``, acceptance
+``(ndim-1) log z + lp(q) - lp(s) > log u'``).  ravest uses ``run_mcmc``,
+``sample`` (its convergence loop), ``iteration``, ``get_autocorr_time(tol=0)``,
+``get_chain`` and ``get_log_prob``; emcee is not installed in this image, so
+two samplers provide that interface here:
 
 * ``EnsembleSampler`` -- host loop around a batched log-probability (e.g.
   ``LogPosterior.log_probability_batch``, whose likelihood runs on the GPU);
@@ -15,16 +17,149 @@ move here, with emcee's chain layout (steps, walkers, ndim) and accessors:
   chain.
 * ``DeviceEnsembleSampler`` -- the whole step on the GPU (rvk_stretch_run,
   include/rvk_post.h): proposals, priors, likelihood, acceptance and the chain
-  stay in HBM.  ``rng="emcee"`` feeds it the same host-drawn stream (same chain
-  as ``EnsembleSampler``); ``rng="philox"`` (default) draws on the device
-  (counter-based Philox; halves [0, W/2) / [W/2, W), emcee 2's split), with no
-  host work per step.
+  stay in HBM; chunks of steps are copied to the host on a copy stream while
+  the next chunk runs.  ``rng="emcee"`` feeds it the same host-drawn stream
+  (same chain as ``EnsembleSampler``); ``rng="philox"`` (default) draws on the
+  device (counter-based Philox, emcee 3's randomised balanced split per step),
+  with no host work per step.
+
+The chain accessors follow emcee 3.1's backend (``get_value``: rows
+``[discard + thin - 1 : iteration : thin]``) and its integrated
+autocorrelation time (``emcee.autocorr.integrated_time``: FFT autocovariance
+per walker, averaged over walkers, Sokal's window with c = 5) is restated in
+``integrated_time`` below.
 """
 from __future__ import annotations
 
+import logging
 import os
 
 import numpy as np
+
+logger = logging.getLogger(__name__)
+
+
+# ---- emcee 3.1 pieces restated (emcee/state.py, emcee/autocorr.py, emcee/ensemble.py) ------------
+
+class State:
+    """emcee.State: the walkers' coordinates and log-probabilities after a step.  Unpacks as
+    ``coords, log_prob, random_state`` (emcee 3's iteration protocol, no blobs)."""
+    __slots__ = ("coords", "log_prob", "blobs", "random_state")
+
+    def __init__(self, coords, log_prob=None, blobs=None, random_state=None, copy=False) -> None:
+        if isinstance(coords, State):
+            coords, log_prob, blobs, random_state = coords.coords, coords.log_prob, coords.blobs, coords.random_state
+        self.coords = np.array(coords, copy=True) if copy else np.atleast_2d(coords)
+        self.log_prob = None if log_prob is None else (np.array(log_prob, copy=True) if copy else log_prob)
+        self.blobs = blobs
+        self.random_state = random_state
+
+    def __len__(self) -> int:
+        return 3 if self.blobs is None else 4
+
+    def __iter__(self):
+        if self.blobs is None:
+            return iter((self.coords, self.log_prob, self.random_state))
+        return iter((self.coords, self.log_prob, self.random_state, self.blobs))
+
+    def __repr__(self) -> str:
+        return f"State({self.coords}, log_prob={self.log_prob}, blobs={self.blobs}, random_state={self.random_state})"
+
+
+class AutocorrError(Exception):
+    """emcee.autocorr.AutocorrError: the chain is too short to estimate tau reliably."""
+
+    def __init__(self, tau, *args, **kwargs):
+        self.tau = tau
+        super().__init__(*args, **kwargs)
+
+
+def next_pow_two(n: int) -> int:
+    i = 1
+    while i < n:
+        i = i << 1
+    return i
+
+
+def function_1d(x) -> np.ndarray:
+    """Normalised autocorrelation function of a 1-D series (emcee.autocorr.function_1d)."""
+    x = np.atleast_1d(x)
+    if len(x.shape) != 1:
+        raise ValueError("invalid dimensions for 1D autocorrelation function")
+    n = next_pow_two(len(x))
+    f = np.fft.fft(x - np.mean(x), n=2 * n)
+    acf = np.fft.ifft(f * np.conjugate(f))[: len(x)].real
+    acf /= acf[0]
+    return acf
+
+
+def _acf_walker_mean(x: np.ndarray, block: int = 256) -> np.ndarray:
+    """Mean over walkers of function_1d of each walker's series: x [n_t, n_w] -> [n_t].  Batched
+    FFTs over blocks of walkers (same arithmetic per walker as function_1d)."""
+    n_t, n_w = x.shape
+    n = next_pow_two(n_t)
+    f = np.zeros(n_t)
+    for k0 in range(0, n_w, block):
+        xb = x[:, k0:k0 + block]
+        F = np.fft.fft(xb - np.mean(xb, axis=0), n=2 * n, axis=0)
+        acf = np.fft.ifft(F * np.conjugate(F), axis=0)[:n_t].real
+        acf /= acf[0]
+        for k in range(acf.shape[1]):        # emcee's order: f += acf of walker k
+            f += acf[:, k]
+    return f / n_w
+
+
+def auto_window(taus, c) -> int:
+    m = np.arange(len(taus)) < c * taus
+    if np.any(m):
+        return int(np.argmin(m))
+    return len(taus) - 1
+
+
+def integrated_time(x, c=5, tol=50, quiet=False) -> np.ndarray:
+    """emcee.autocorr.integrated_time: x [n_steps, n_walkers, n_dim] (or 1-D / 2-D) -> tau [n_dim].
+    Raises AutocorrError when tol * tau > n_steps unless quiet (then logs a warning); tol=0
+    (ravest's call, fit.py:1131) never raises."""
+    x = np.atleast_1d(x)
+    if len(x.shape) == 1:
+        x = x[:, np.newaxis, np.newaxis]
+    if len(x.shape) == 2:
+        x = x[:, :, np.newaxis]
+    if len(x.shape) != 3:
+        raise ValueError("invalid dimensions")
+    n_t, n_w, n_d = x.shape
+    tau_est = np.empty(n_d)
+    windows = np.empty(n_d, dtype=int)
+    for d in range(n_d):
+        f = _acf_walker_mean(np.asarray(x[:, :, d], dtype=np.float64))
+        taus = 2.0 * np.cumsum(f) - 1.0
+        windows[d] = auto_window(taus, c)
+        tau_est[d] = taus[windows[d]]
+    flag = tol * tau_est > n_t
+    if np.any(flag):
+        msg = ("The chain is shorter than {0} times the integrated autocorrelation time for {1} parameter(s). "
+               "Use this estimate with caution and run a longer chain!\n").format(tol, np.sum(flag))
+        msg += "N/{0} = {1:.0f};\ntau: {2}".format(tol, n_t / tol, tau_est)
+        if not quiet:
+            raise AutocorrError(tau_est, msg)
+        logger.warning(msg)
+    return tau_est
+
+
+def walkers_independent(coords) -> bool:
+    """emcee.ensemble.walkers_independent: finite, no constant coordinate, and the centred,
+    scaled walker matrix has condition number <= 1e8."""
+    coords = np.asarray(coords, dtype=np.float64)
+    if not np.all(np.isfinite(coords)):
+        return False
+    C = coords - np.mean(coords, axis=0)[None, :]
+    C_colmax = np.amax(np.abs(C), axis=0)
+    if np.any(C_colmax == 0):
+        return False
+    C /= C_colmax
+    C_colsum = np.sqrt(np.sum(C ** 2, axis=0))
+    C /= C_colsum
+    return bool(np.linalg.cond(C.astype(float)) <= 1e8)
 
 
 def emcee_step_draws(random: np.random.RandomState, nwalkers: int):
@@ -59,37 +194,143 @@ def _random_state(seed):
     return np.random.RandomState(seed)
 
 
-class _ChainMixin:
+class _Backend:
+    """emcee.backends.Backend (in memory): chain [n, W, D], log_prob [n, W], accepted [W] and the
+    iteration count; grown ahead of a run, read through get_value's slicing."""
+
+    def __init__(self, nwalkers: int, ndim: int) -> None:
+        self.nwalkers, self.ndim = nwalkers, ndim
+        self.reset()
+
     def reset(self) -> None:
-        self._chain, self._lnp = [], []
-        self.naccepted = np.zeros(self.nwalkers, dtype=np.int64)
         self.iteration = 0
+        self.accepted = np.zeros(self.nwalkers, dtype=np.int64)
+        self.chain = np.empty((0, self.nwalkers, self.ndim))
+        self.log_prob = np.empty((0, self.nwalkers))
+
+    def grow(self, ngrow: int) -> None:
+        need = self.iteration + ngrow
+        if need <= len(self.chain):
+            return
+        chain = np.empty((need, self.nwalkers, self.ndim))       # untouched pages cost nothing
+        lnp = np.empty((need, self.nwalkers))
+        chain[:self.iteration] = self.chain[:self.iteration]
+        lnp[:self.iteration] = self.log_prob[:self.iteration]
+        self.chain, self.log_prob = chain, lnp
+
+    def get_value(self, name: str, flat=False, thin=1, discard=0):
+        if self.iteration <= 0:
+            raise AttributeError("you must run the sampler with 'store == True' before accessing the results")
+        v = getattr(self, name)[discard + thin - 1:self.iteration:thin]
+        if flat:
+            return v.reshape((-1,) + v.shape[2:])
+        return v
+
+
+class _SamplerBase:
+    """emcee.EnsembleSampler's accessors over a _Backend."""
+
+    def reset(self) -> None:
+        self.backend.reset()
+
+    @property
+    def iteration(self) -> int:
+        return self.backend.iteration
+
+    @property
+    def naccepted(self) -> np.ndarray:
+        return self.backend.accepted
 
     @property
     def acceptance_fraction(self) -> np.ndarray:
-        return self.naccepted / max(1, self.iteration)
+        return self.naccepted / float(self.iteration)
 
-    def get_chain(self, discard: int = 0, thin: int = 1, flat: bool = False) -> np.ndarray:
-        ch = (np.concatenate(self._chain) if self._chain else np.zeros((0, self.nwalkers, self.ndim)))[discard::thin]
-        return ch.reshape(-1, self.ndim) if flat else ch
+    def get_chain(self, flat=False, thin=1, discard=0) -> np.ndarray:
+        return self.backend.get_value("chain", flat=flat, thin=thin, discard=discard)
 
-    def get_log_prob(self, discard: int = 0, thin: int = 1, flat: bool = False) -> np.ndarray:
-        lp = (np.concatenate(self._lnp) if self._lnp else np.zeros((0, self.nwalkers)))[discard::thin]
-        return lp.reshape(-1) if flat else lp
+    def get_log_prob(self, flat=False, thin=1, discard=0) -> np.ndarray:
+        return self.backend.get_value("log_prob", flat=flat, thin=thin, discard=discard)
 
-    def _check_init(self, x, nwalkers, ndim):
-        if x.shape != (nwalkers, ndim):
-            raise ValueError(f"initial_state must have shape ({nwalkers}, {ndim})")
+    def get_blobs(self, **kwargs):
+        return None
+
+    @property
+    def chain(self) -> np.ndarray:
+        return np.swapaxes(self.get_chain(), 0, 1)
+
+    @property
+    def flatchain(self) -> np.ndarray:
+        return self.get_chain(flat=True)
+
+    @property
+    def lnprobability(self) -> np.ndarray:
+        return np.swapaxes(self.get_log_prob(), 0, 1)
+
+    def get_autocorr_time(self, discard=0, thin=1, **kwargs) -> np.ndarray:
+        """emcee: thin * integrated_time(get_chain(discard, thin), **kwargs)."""
+        return thin * integrated_time(self.get_chain(discard=discard, thin=thin), **kwargs)
+
+    def get_last_sample(self) -> State:
+        it = self.iteration
+        if it <= 0:
+            raise AttributeError("you must run the sampler with 'store == True' before accessing the results")
+        return State(self.get_chain(discard=it - 1)[0], log_prob=self.get_log_prob(discard=it - 1)[0],
+                     random_state=getattr(self, "_last_random_state", None))
+
+    def _initial(self, initial_state, log_prob0, skip_initial_state_check):
+        """emcee's checks of the initial state (EnsembleSampler.sample)."""
+        if initial_state is None:
+            prev = getattr(self, "_previous_state", None)
+            if prev is None:
+                raise ValueError("Cannot have `initial_state=None` if run_mcmc has never been called.")
+            return prev
+        st = State(initial_state, copy=True)
+        if log_prob0 is not None:
+            st.log_prob = np.array(log_prob0, dtype=np.float64, copy=True)
+        st.coords = np.asarray(st.coords, dtype=np.float64)
+        if np.shape(st.coords) != (self.nwalkers, self.ndim):
+            raise ValueError(f"incompatible input dimensions: initial_state must have shape "
+                             f"({self.nwalkers}, {self.ndim})")
+        if not skip_initial_state_check and not walkers_independent(st.coords):
+            raise ValueError("Initial state has a large condition number. Make sure that your walkers are linearly "
+                             "independent for the best performance")
+        return st
 
     @staticmethod
-    def _check_init_lnp(lnp):
+    def _check_initial_log_prob(lnp) -> None:
         if np.any(np.isnan(lnp)):
             raise ValueError("The initial log_prob was NaN")
-        if not np.all(np.isfinite(lnp)):
-            raise ValueError("Initial state has walkers with -inf log-probability")
+
+    @staticmethod
+    def _unsupported(thin_by, thin, blobs0) -> None:
+        if thin is not None or thin_by != 1:
+            raise NotImplementedError("thinned storage (thin_by / thin) is not supported; thin at read time "
+                                      "with get_chain(thin=...)")
+        if blobs0 is not None:
+            raise NotImplementedError("blobs are not supported (ravest's log-probabilities have none)")
+
+    def run_mcmc(self, initial_state, nsteps: int, **kwargs):
+        """emcee: iterate sample() for nsteps steps; returns the last State."""
+        results = None
+        for results in self.sample(initial_state, iterations=nsteps, **kwargs):
+            pass
+        return results
 
 
-class EnsembleSampler(_ChainMixin):
+def _progress_bar(progress, total):
+    if not progress:
+        return None
+    try:
+        import tqdm
+    except ImportError:
+        return None
+    return tqdm.tqdm(total=total, **(progress if isinstance(progress, dict) else {}))
+
+
+class EnsembleSampler(_SamplerBase):
+    """emcee's stretch move on the host over a batched log-probability (``vectorize=True`` form:
+    ``log_prob_batch([W/2, D]) -> [W/2]``), emcee's RandomState call order."""
+
     def __init__(self, nwalkers: int, ndim: int, log_prob_batch, a: float = 2.0, seed=None) -> None:
         if nwalkers < 2 * ndim:
             raise ValueError(f"nwalkers ({nwalkers}) must be at least 2 * ndim ({2 * ndim})")
@@ -98,15 +339,29 @@ class EnsembleSampler(_ChainMixin):
         self.nwalkers, self.ndim, self.a = nwalkers, ndim, float(a)
         self.log_prob_batch = log_prob_batch
         self.random = _random_state(seed)
-        self.reset()
+        self.backend = _Backend(nwalkers, ndim)
+        self._previous_state = None
 
-    def sample(self, initial_state, iterations: int):
-        x = np.array(initial_state, dtype=np.float64, copy=True)
-        self._check_init(x, self.nwalkers, self.ndim)
-        lnp = np.asarray(self.log_prob_batch(x), dtype=np.float64)
-        self._check_init_lnp(lnp)
+    @property
+    def random_state(self):
+        return self.random.get_state()
+
+    def sample(self, initial_state=None, log_prob0=None, rstate0=None, blobs0=None, iterations=1, tune=False,
+               skip_initial_state_check=False, thin_by=1, thin=None, store=True, progress=False, progress_kwargs=None):
+        self._unsupported(thin_by, thin, blobs0)
+        st = self._initial(initial_state, log_prob0, skip_initial_state_check)
+        if rstate0 is not None:
+            self.random.set_state(rstate0)
+        x = np.array(st.coords, dtype=np.float64, copy=True)
+        lnp = (np.asarray(self.log_prob_batch(x), dtype=np.float64) if st.log_prob is None
+               else np.array(st.log_prob, dtype=np.float64, copy=True))
+        self._check_initial_log_prob(lnp)
+        if store:
+            self.backend.grow(iterations)
+        bar = _progress_bar(progress, iterations)
         for _ in range(iterations):
             sets, zu, rint, au = emcee_step_draws(self.random, self.nwalkers)
+            accepted = np.zeros(self.nwalkers, dtype=bool)
             for split in (0, 1):
                 S, Cc = sets[split], sets[1 - split]
                 s, c = x[S], x[Cc]
@@ -115,34 +370,217 @@ class EnsembleSampler(_ChainMixin):
                 q = c[rint[split]] - (c[rint[split]] - s) * zz[:, None]
                 new = np.asarray(self.log_prob_batch(q), dtype=np.float64)
                 if np.any(np.isnan(new)):
-                    raise ValueError("The log_prob was NaN")   # emcee: -inf rejects, NaN raises
+                    raise ValueError("Probability function returned NaN")   # emcee: -inf rejects, NaN raises
                 lnpdiff = factors + new - lnp[S]
                 acc = lnpdiff > np.log(au[split])
                 x[S[acc]] = q[acc]
                 lnp[S[acc]] = new[acc]
-                self.naccepted[S[acc]] += 1
-            self.iteration += 1
-            self._chain.append(x[None].copy())
-            self._lnp.append(lnp[None].copy())
-            yield x, lnp
+                accepted[S[acc]] = True
+            b = self.backend
+            if store:
+                b.chain[b.iteration] = x
+                b.log_prob[b.iteration] = lnp
+            b.accepted += accepted
+            b.iteration += 1
+            self._previous_state = State(x, log_prob=lnp, random_state=self.random.get_state(), copy=True)
+            if bar is not None:
+                bar.update(1)
+            yield State(x, log_prob=lnp, random_state=self.random.get_state(), copy=True)
+        if bar is not None:
+            bar.close()
 
-    def run_mcmc(self, initial_state, nsteps: int):
-        state = None
-        for state in self.sample(initial_state, nsteps):
-            pass
-        return state
+
+class _Chunk:
+    """One chunk of device steps in flight: where it starts, its copy-out slot and events, and what
+    its sampler needs to resume exactly at any step inside it."""
+    __slots__ = ("start", "n", "slot", "copied", "x0", "lp0", "nacc0", "draws", "rstate0")
 
 
-class DeviceEnsembleSampler(_ChainMixin):
+class _DevicePipeline(_SamplerBase):
+    """emcee's EnsembleSampler.sample over chunks of device steps.  The walker state, the draws and
+    each chunk's chain stay in device memory; a finished chunk is copied to pinned host memory on
+    a copy stream while the next chunk runs, then into the backend's arrays, and its steps are
+    yielded one by one.  Subclasses provide the steps (_run_chunk), what a chunk must record to be
+    resumed inside (_begin_chunk) and the rewind to a step inside the last chunks (_settle,
+    naccepted)."""
+
+    def _pipeline_init(self, device, keep_host: bool = True) -> None:
+        import torch
+        self.device = device
+        self.backend = _Backend(self.nwalkers, self.ndim)
+        self._keep_host = keep_host          # copy the chain to this process's host memory
+        self._token = 0
+        self._x = self._lp = None            # device state, at step self._dev_iter
+        self._nacc = torch.zeros(self.nwalkers, dtype=torch.int64, device=device)
+        self._status = torch.zeros(1, dtype=torch.int32, device=device)
+        self._dev_iter = 0
+        self._chunks = []                    # the last chunks (the committed step lies in them)
+        self._dbuf = [None, None]            # device chain / log-prob buffers, per slot
+        self._stage = [None, None]           # pinned host staging, per slot
+        self._copy_stream = None
+        self._nslot = 0
+        self._accepted_iter = 0              # backend.accepted is exact at this iteration
+
+    @property
+    def _cuda(self) -> bool:
+        return self.device.type == "cuda"
+
+    def _stream(self):
+        import torch
+        return torch.cuda.current_stream(self.device) if self._cuda else None
+
+    def _ensure_buffers(self, slot: int) -> None:
+        import torch
+        if self._dbuf[slot] is not None:
+            return
+        n, W, D = self.steps_per_call, self.nwalkers, self.ndim
+        self._dbuf[slot] = (torch.empty((n, W, D), dtype=torch.float64, device=self.device),
+                            torch.empty((n, W), dtype=torch.float64, device=self.device))
+        if self._cuda:
+            pin = dict(pin_memory=True)
+            self._stage[slot] = (torch.empty((n, W, D), dtype=torch.float64, **pin) if self._keep_host else None,
+                                 torch.empty((n, W), dtype=torch.float64, **pin) if self._keep_host else None,
+                                 torch.empty(1, dtype=torch.int32, **pin))
+            if self._copy_stream is None:
+                self._copy_stream = torch.cuda.Stream(self.device)
+        else:                                 # host tensors: the device buffers are the staging
+            self._stage[slot] = (self._dbuf[slot][0], self._dbuf[slot][1], self._status)
+
+    def reset(self) -> None:
+        self.backend.reset()
+        self._x = self._lp = None
+        self._nacc.zero_()
+        self._dev_iter = 0
+        self._chunks = []
+        self._accepted_iter = 0
+        self._token += 1
+
+    def _set_state(self, st: State) -> None:
+        import torch
+        self._x = torch.from_numpy(np.ascontiguousarray(st.coords, dtype=np.float64)).to(self.device)
+        self._lp = torch.empty(self.nwalkers, dtype=torch.float64, device=self.device)
+        if st.log_prob is None:
+            self._initial_log_prob(self._x, self._lp)
+        else:
+            self._lp.copy_(torch.from_numpy(np.ascontiguousarray(st.log_prob, dtype=np.float64)))
+        self._check_initial_log_prob(self._lp.cpu().numpy())
+        self._dev_iter = self.iteration
+        self._x_init = (self._dev_iter, self._x.clone(), self._lp.clone(), self._nacc.clone())
+        self._chunks = []
+
+    def _enqueue(self, n: int) -> _Chunk:
+        import torch
+        stream = self._stream()
+        slot = self._nslot % 2
+        self._nslot += 1
+        self._ensure_buffers(slot)
+        prev = next((c for c in reversed(self._chunks) if c.slot == slot), None)
+        if prev is not None and prev.copied is not None:
+            stream.wait_event(prev.copied)    # the slot's device buffers were being copied out
+        ch = _Chunk()
+        ch.start, ch.n, ch.slot, ch.copied = self._dev_iter, n, slot, None
+        self._begin_chunk(ch)
+        chain_d, lnp_d = self._dbuf[slot]
+        self._run_chunk(ch, chain_d, lnp_d, stream)
+        self._dev_iter += n
+        if self._cuda:
+            computed = torch.cuda.Event()
+            computed.record(stream)
+            cs = self._copy_stream
+            cs.wait_event(computed)
+            with torch.cuda.stream(cs):
+                sc, sl, ss = self._stage[slot]
+                if self._keep_host:
+                    sc[:n].copy_(chain_d[:n], non_blocking=True)
+                    sl[:n].copy_(lnp_d[:n], non_blocking=True)
+                ss.copy_(self._status, non_blocking=True)
+            ch.copied = torch.cuda.Event()
+            ch.copied.record(cs)
+        else:                                 # host tensors: the chunk's status as it ended
+            self._stage[slot] = (chain_d, lnp_d, self._status.clone())
+        self._chunks = (self._chunks + [ch])[-3:]
+        return ch
+
+    def sample(self, initial_state=None, log_prob0=None, rstate0=None, blobs0=None, iterations=1, tune=False,
+               skip_initial_state_check=False, thin_by=1, thin=None, store=True, progress=False, progress_kwargs=None):
+        """emcee's EnsembleSampler.sample: yields a State per step (``iteration`` counts them)."""
+        import torch
+        self._unsupported(thin_by, thin, blobs0)
+        self._settle()
+        self._token += 1
+        tok = self._token
+        if initial_state is None:
+            if self._x is None:
+                raise ValueError("Cannot have `initial_state=None` if run_mcmc has never been called.")
+        else:
+            st = self._initial(initial_state, log_prob0, skip_initial_state_check)
+            if rstate0 is not None and getattr(self, "rng", None) == "emcee":
+                self.random.set_state(rstate0)
+            self._set_state(st)
+        store = store and self._keep_host
+        if store:
+            self.backend.grow(iterations)
+        bar = _progress_bar(progress, iterations)
+        done, pending = 0, None
+        while True:
+            nxt = None
+            if done < iterations:
+                nxt = self._enqueue(min(self.steps_per_call, iterations - done))
+                done += nxt.n
+            if pending is not None:
+                if pending.copied is not None:
+                    pending.copied.synchronize()
+                sc, sl, ss = self._stage[pending.slot]
+                if int(ss[0]):
+                    self._status.zero_()
+                    raise ValueError("Probability function returned NaN")
+                b = self.backend
+                a, e = pending.start, pending.start + pending.n
+                if store:                     # multi-threaded copy out of the pinned staging
+                    torch.from_numpy(b.chain[a:e]).copy_(sc[:pending.n])
+                    torch.from_numpy(b.log_prob[a:e]).copy_(sl[:pending.n])
+                for i in range(pending.n):
+                    if tok != self._token:
+                        raise RuntimeError("this sample() generator was superseded by a later sample()/run_mcmc()/"
+                                           "reset() call")
+                    t = a + i
+                    b.iteration = t + 1
+                    if store:
+                        state = State(b.chain[t], log_prob=b.log_prob[t])
+                    elif sc is not None:
+                        state = State(sc[i].numpy(), log_prob=sl[i].numpy(), copy=True)
+                    else:
+                        state = State(np.empty((0, self.ndim)))   # this rank keeps no chain
+                    if bar is not None:
+                        bar.update(1)
+                    yield state
+            if nxt is None:
+                break
+            pending = nxt
+        if bar is not None:
+            bar.close()
+
+
+class DeviceEnsembleSampler(_DevicePipeline):
     """The stretch move with every sub-step on the GPU (include/rvk_post.h rvk_stretch_run).
 
     ``log_posterior`` is a ``posterior.LogPosterior`` (or its ``DevicePosterior``), or a
     ``gp.GPLogPosterior`` (or its ``DeviceGPPosterior``: GPFitter.run_mcmc's sampler,
-    rvk_gp_stretch_run); its priors must be built-in prior classes.  The walker state,
-    the chain and the log-probabilities live in HBM; ``get_chain`` copies them to the host."""
+    rvk_gp_stretch_run); its priors must be built-in prior classes.  emcee 3.1's interface
+    (``sample``, ``run_mcmc``, ``iteration``, ``get_chain``, ``get_log_prob``,
+    ``get_autocorr_time``, ``acceptance_fraction``, ``get_last_sample``).
+
+    Steps run in chunks of ``steps_per_call`` on the device (state, draws and the chunk's chain
+    in HBM); each finished chunk is copied to pinned host memory on a copy stream while the next
+    chunk runs, and ``sample`` yields its steps one by one.  A consumer that stops early (ravest's
+    convergence break) leaves the device up to one chunk ahead: the next call (and
+    ``naccepted``) replays the chunk from its start up to ``iteration`` -- the draws depend only
+    on (seed, global step), so the replay is exact and a run split over several calls is the
+    same chain as one call.  A NaN log-probability raises ValueError at the chunk it occurs in,
+    before any of that chunk's steps is yielded (emcee raises at the step)."""
 
     def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed=None, rng: str = "philox",
-                 steps_per_call: int = 256) -> None:
+                 steps_per_call: int = 256, randomize_split: bool = True) -> None:
         import torch
         from .gp import DeviceGPPosterior, GPLogPosterior
         from .posterior import DevicePosterior
@@ -161,53 +599,86 @@ class DeviceEnsembleSampler(_ChainMixin):
         if rng not in ("philox", "emcee"):
             raise ValueError("rng must be 'philox' (device) or 'emcee' (host RandomState stream)")
         self.nwalkers, self.ndim, self.a, self.rng = nwalkers, ndim, float(a), rng
-        self.steps_per_call = int(steps_per_call)
-        self.device = torch.device("cuda", torch.cuda.current_device())
+        self.randomize_split = bool(randomize_split)
+        self.steps_per_call = max(1, int(steps_per_call))
         if rng == "emcee":
             self.random = _random_state(seed)
+            if not self.randomize_split:
+                raise ValueError("rng='emcee' draws emcee's randomised split; randomize_split=False needs rng='philox'")
         else:
             self.seed = int(seed) if seed is not None else int.from_bytes(os.urandom(8), "little")
         self.post.reserve(nwalkers)
-        self.reset()
+        self._pipeline_init(torch.device("cuda", torch.cuda.current_device()))
 
-    def run_mcmc(self, initial_state, nsteps: int):
-        import torch
+    def _flags(self) -> int:
         from . import _lib
-        W, D = self.nwalkers, self.ndim
-        x0 = np.array(initial_state, dtype=np.float64, copy=True)
-        self._check_init(x0, W, D)
-        dev = self.device
-        x = torch.from_numpy(x0).to(dev)
-        lp = torch.empty(W, dtype=torch.float64, device=dev)
-        stream = torch.cuda.current_stream(dev)
-        self.post.device(x, lp, stream)
-        self._check_init_lnp(lp.cpu().numpy())
-        nacc = torch.zeros(W, dtype=torch.int64, device=dev)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        return 0 if self.randomize_split else _lib.STRETCH_FIXED_SPLIT
+
+    def _initial_log_prob(self, x, lp) -> None:
+        self.post.device(x, lp, self._stream())
+
+    def _host_draws(self, n: int):
+        import torch
+        steps = [emcee_step_draws(self.random, self.nwalkers) for _ in range(n)]
+        return [torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in steps]))).to(self.device)
+                for k in range(4)]
+
+    def _launch(self, x, lp, nacc, n, step0, draws, chain_d, lnp_d, stream) -> None:
+        from . import _lib
         L = _lib.load()
-        done = 0
-        while done < nsteps:
-            n = min(self.steps_per_call, nsteps - done)
-            chain = torch.empty((n, W, D), dtype=torch.float64, device=dev)
-            lnpc = torch.empty((n, W), dtype=torch.float64, device=dev)
-            draws = None
-            if self.rng == "emcee":
-                steps = [emcee_step_draws(self.random, W) for _ in range(n)]
-                draws = [torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in steps]))).to(dev)
-                         for k in range(4)]
-            ptr = (lambda t: t.data_ptr()) if draws else (lambda t: 0)
-            _lib.check(getattr(L, self._run_fn)(self.post._p, x.data_ptr(), lp.data_ptr(), W, n, self.a,
-                                         getattr(self, "seed", 0), self.iteration + done,
-                                         ptr(draws[0]) if draws else 0, ptr(draws[1]) if draws else 0,
-                                         ptr(draws[2]) if draws else 0, ptr(draws[3]) if draws else 0,
-                                         chain.data_ptr(), lnpc.data_ptr(), nacc.data_ptr(), status.data_ptr(),
-                                         stream.cuda_stream))
-            if int(status.item()):
-                raise ValueError("The log_prob was NaN")
-            self._chain.append(chain.cpu().numpy())
-            self._lnp.append(lnpc.cpu().numpy())
-            done += n
-        self.iteration += nsteps
-        self.naccepted += nacc.cpu().numpy()
-        self.state = (x.cpu().numpy(), lp.cpu().numpy())
-        return self.state
+        d = [t.data_ptr() for t in draws] if draws else [0, 0, 0, 0]
+        _lib.check(getattr(L, self._run_fn)(self.post._p, x.data_ptr(), lp.data_ptr(), self.nwalkers, n, self.a,
+                                            getattr(self, "seed", 0), step0, self._flags(), d[0], d[1], d[2], d[3],
+                                            0 if chain_d is None else chain_d.data_ptr(),
+                                            0 if lnp_d is None else lnp_d.data_ptr(), nacc.data_ptr(),
+                                            self._status.data_ptr(), stream.cuda_stream))
+
+    def _begin_chunk(self, ch: _Chunk) -> None:
+        ch.x0, ch.lp0, ch.nacc0 = self._x.clone(), self._lp.clone(), self._nacc.clone()
+        ch.rstate0 = self.random.get_state() if self.rng == "emcee" else None
+        ch.draws = self._host_draws(ch.n) if self.rng == "emcee" else None
+
+    def _run_chunk(self, ch: _Chunk, chain_d, lnp_d, stream) -> None:
+        self._launch(self._x, self._lp, self._nacc, ch.n, ch.start, ch.draws, chain_d, lnp_d, stream)
+
+    def _replay_to(self, target: int, x, lp, nacc) -> None:
+        """Device state of step `target` into (x, lp, nacc): from the start of the chunk that
+        holds it, replay the chunk's first target - start steps (same draws)."""
+        ch = next((c for c in self._chunks if c.start <= target <= c.start + c.n), None)
+        if ch is None:
+            raise RuntimeError("internal: no chunk record covers the requested step")
+        x.copy_(ch.x0)
+        lp.copy_(ch.lp0)
+        nacc.copy_(ch.nacc0)
+        k = target - ch.start
+        if k:
+            draws = [t[:k] for t in ch.draws] if ch.draws else None
+            self._launch(x, lp, nacc, k, ch.start, draws, None, None, self._stream())
+
+    def _settle(self) -> None:
+        """Bring the device state back to self.iteration after a generator stopped early."""
+        if self._x is None or self._dev_iter == self.iteration:
+            return
+        self._replay_to(self.iteration, self._x, self._lp, self._nacc)
+        if self.rng == "emcee":
+            ch = next(c for c in self._chunks if c.start <= self.iteration <= c.start + c.n)
+            self.random.set_state(ch.rstate0)
+            for _ in range(self.iteration - ch.start):
+                emcee_step_draws(self.random, self.nwalkers)
+        self._dev_iter = self.iteration
+        self._chunks = []
+        self.backend.accepted = self._nacc.cpu().numpy()
+        self._accepted_iter = self.iteration
+
+    @property
+    def naccepted(self) -> np.ndarray:
+        if self._accepted_iter != self.iteration:
+            if self._dev_iter == self.iteration:
+                self.backend.accepted = self._nacc.cpu().numpy()
+            else:                             # a generator is suspended inside a chunk: replay on scratch
+                import torch
+                x, lp, nacc = torch.empty_like(self._x), torch.empty_like(self._lp), torch.empty_like(self._nacc)
+                self._replay_to(self.iteration, x, lp, nacc)
+                self.backend.accepted = nacc.cpu().numpy()
+            self._accepted_iter = self.iteration
+        return self.backend.accepted

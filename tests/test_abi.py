@@ -58,8 +58,12 @@ def test_bad_arguments_fail_loudly():
     assert not L.rvk_post_create(None, 1, None, None, 0, None, None, None, 0.0, 0.0, 0)
     assert "handle" in _lib.last_error()
     assert L.rvk_logpost_device(None, None, 1, 1, None, None) == -1
-    assert L.rvk_stretch_run(None, None, None, 8, 1, 2.0, 0, 0, None, None, None, None, None, None, None, None,
+    assert L.rvk_stretch_run(None, None, None, 8, 1, 2.0, 0, 0, 0, None, None, None, None, None, None, None, None,
                              None) == -1
+    assert L.rvk_stretch_draws(None, 8, 1, 2.0, 0, 0, 0, None) == -1
+    assert L.rvk_stretch_propose(None, None, 8, 0, 0, 0, 4, None, None) == -1
+    assert L.rvk_stretch_update(None, None, None, 8, 0, 0, None, None, None, None, None, None, None) == -1
+    assert L.rvk_stretch_table_read(None, 0, 0, None, None, None) == -1
     assert not L.rvk_gp_create(None, 0) and "handle" in _lib.last_error()
     assert L.rvk_gp_loglike_device(None, None, None, 1, 9, 4, None, None) == -1
 

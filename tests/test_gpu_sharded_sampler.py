@@ -1,7 +1,9 @@
-"""ShardedDeviceSampler (ravest_amd/distributed.py, include/rvk_post.h rvk_stretch_half): the
-device stretch move split over ranks by proposal slices, with the updated rows all-gathered every
-half-step.  Rehearsed here with 2 ranks on one MI355X over gloo (the 8-GPU RCCL run is the
-driver's); the chain, log-probs and acceptance counts must equal the single-GPU device sampler
+"""ShardedDeviceSampler (ravest_amd/distributed.py, include/rvk_post.h rvk_stretch_draws /
+rvk_stretch_propose / rvk_stretch_update): every rank evaluates a slice of each half-step's
+proposals, the H log-posteriors are all-gathered (H x 8 bytes) and every rank applies the
+accept / reject to the whole half.  One rank on the GPU (the propose / update kernels, no
+collective), two ranks over gloo on one MI355X, and two ranks over RCCL when the box has two
+GPUs; the chain, log-probs and acceptance counts must equal the single-GPU DeviceEnsembleSampler
 with the same Philox seed bit for bit."""
 import os
 import subprocess
@@ -15,36 +17,53 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _single(W, steps):
+def _single(W, steps, randomize=True):
     from ravest_amd.sampler import DeviceEnsembleSampler
     from ravest_amd.synth import make_posterior
     lpost, x0 = make_posterior(2, W, seed=4)
-    s = DeviceEnsembleSampler(lpost, W, seed=77, steps_per_call=5)
+    s = DeviceEnsembleSampler(lpost, W, seed=77, steps_per_call=5, randomize_split=randomize)
     s.run_mcmc(x0, steps)
     return s
 
 
-def test_sharded_sampler_one_rank_equals_single_gpu():
+@pytest.mark.parametrize("randomize", [True, False])
+def test_sharded_sampler_one_rank_equals_single_gpu(randomize):
     import torch.distributed as dist
     from ravest_amd.distributed import ShardedDeviceSampler
     from ravest_amd.synth import make_posterior
     assert not (dist.is_available() and dist.is_initialized())
     W, steps = 256, 12
     lpost, x0 = make_posterior(2, W, seed=4)
-    sh = ShardedDeviceSampler(lpost, W, seed=77)
+    sh = ShardedDeviceSampler(lpost, W, seed=77, steps_per_call=4, randomize_split=randomize)
     sh.run_mcmc(x0, steps)
-    ref = _single(W, steps)
+    ref = _single(W, steps, randomize)
     assert np.array_equal(sh.get_chain(), ref.get_chain())
     assert np.array_equal(sh.get_log_prob(), ref.get_log_prob())
     assert np.array_equal(sh.naccepted, ref.naccepted)
+    assert sh.exchange_bytes_per_half_step == (W // 2) * 8
 
 
-def test_sharded_sampler_two_ranks_gloo(tmp_path):
-    W, steps = 256, 10
-    out = tmp_path / "chain.npz"
-    env = dict(os.environ, RVK_TEST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+def test_sharded_sampler_rejects_gp_posterior():
+    from ravest_amd.distributed import ShardedDeviceSampler
+    from ravest_amd.gp import GPKernel, GPLogPosterior
+    from ravest_amd.synth import make_dataset
+    from ravest_amd import prior as P
+    ds = make_dataset(1, 40, 1, seed=3)
+    free = ["P_b", "K_b"]
+    fixed = {n: float(ds.truth[n]) for n in ds.names if n not in free}
+    gp = GPLogPosterior(ds.planet_letters, ds.parameterisation, GPKernel("Quasiperiodic"),
+                        {"P_b": P.Uniform(1, 100), "K_b": P.Uniform(0, 100)}, {},
+                        fixed, {"gp_amp": 2.0, "gp_lambda_e": 50.0, "gp_lambda_p": 0.5, "gp_period": 20.0}, free, [],
+                        ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments)
+    with pytest.raises(TypeError, match="GP posterior"):
+        ShardedDeviceSampler(gp, 16)
+
+
+def _run_ranks(tmp_path, backend, port, W=256, steps=10):
+    out = tmp_path / f"chain_{backend}.npz"
+    env = dict(os.environ, RVK_TEST_BACKEND=backend, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29533", os.path.join(ROOT, "tests", "_sharded_sampler_worker.py"),
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "_sharded_sampler_worker.py"),
            str(out), str(W), str(steps)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -53,4 +72,16 @@ def test_sharded_sampler_two_ranks_gloo(tmp_path):
     assert np.array_equal(got["chain"], ref.get_chain())
     assert np.array_equal(got["lnp"], ref.get_log_prob())
     assert np.array_equal(got["nacc"], ref.naccepted)
+    assert int(got["xbytes"]) == (W // 2) * 8
     assert got["nacc"].sum() > 0
+
+
+def test_sharded_sampler_two_ranks_gloo(tmp_path):
+    _run_ranks(tmp_path, "gloo", 29533)
+
+
+def test_sharded_sampler_two_ranks_rccl(tmp_path):
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("the RCCL form needs two GPUs (the driver's 8-GPU node)")
+    _run_ranks(tmp_path, "nccl", 29534)

@@ -2,7 +2,8 @@
 import numpy as np
 import pytest
 
-from ravest_amd.sampler import EnsembleSampler, emcee_step_draws
+from ravest_amd.sampler import (AutocorrError, EnsembleSampler, State, emcee_step_draws, function_1d,
+                                integrated_time, walkers_independent)
 
 
 def test_gaussian_moments():
@@ -32,8 +33,13 @@ def test_minus_inf_rejects_nan_raises():
     s.run_mcmc(np.random.default_rng(1).uniform(-0.5, 0.5, (8, 2)), 200)
     assert np.all(s.get_chain()[:, :, 0] <= 1.0)
     s2 = EnsembleSampler(8, 2, lambda x: np.full(len(x), np.nan), seed=3)
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError, match="initial log_prob was NaN"):
+        s2.run_mcmc(np.random.default_rng(1).uniform(-0.5, 0.5, (8, 2)), 1)
+    with pytest.raises(ValueError, match="condition number"):     # emcee's walkers_independent check
         s2.run_mcmc(np.zeros((8, 2)), 1)
+    s3 = EnsembleSampler(8, 2, lambda x: np.where(x[:, 0] > 0.4, np.nan, -0.5 * np.sum(x ** 2, axis=1)), seed=3)
+    with pytest.raises(ValueError, match="Probability function returned NaN"):
+        s3.run_mcmc(np.random.default_rng(1).uniform(-0.5, 0.3, (8, 2)), 50)
 
 
 def test_emcee_call_order():
@@ -51,3 +57,92 @@ def test_emcee_call_order():
         assert np.array_equal(rint[split], b.randint(H, size=(H,)))
         assert np.array_equal(au[split], np.array([b.rand() for _ in range(H)]))
     assert np.array_equal(np.sort(np.concatenate(sets)), np.arange(W))
+
+
+def _emcee_integrated_time_literal(x, c=5):
+    """emcee 3.1's integrated_time, literally (one function_1d per walker, summed in order)."""
+    n_t, n_w, n_d = x.shape
+    tau = np.empty(n_d)
+    for d in range(n_d):
+        f = np.zeros(n_t)
+        for k in range(n_w):
+            f += function_1d(x[:, k, d])
+        f /= n_w
+        taus = 2.0 * np.cumsum(f) - 1.0
+        m = np.arange(len(taus)) < c * taus
+        w = np.argmin(m) if np.any(m) else len(taus) - 1
+        tau[d] = taus[w]
+    return tau
+
+
+def test_integrated_time_matches_emcee():
+    rng = np.random.default_rng(3)
+    # AR(1) walkers with known tau = (1 + phi) / (1 - phi)
+    phi = np.array([0.5, 0.9])
+    n_t, n_w = 4000, 300
+    x = np.zeros((n_t, n_w, 2))
+    e = rng.standard_normal((n_t, n_w, 2))
+    for t in range(1, n_t):
+        x[t] = phi * x[t - 1] + e[t]
+    tau = integrated_time(x, tol=0)
+    assert np.allclose(tau, _emcee_integrated_time_literal(x), rtol=1e-12, atol=0)
+    assert np.allclose(tau, (1 + phi) / (1 - phi), rtol=0.1)
+    with pytest.raises(AutocorrError):
+        integrated_time(x[:200], tol=50)
+    assert np.all(np.isfinite(integrated_time(x[:200], tol=50, quiet=True)))
+
+
+def test_chain_accessors_follow_emcee_backend():
+    s = EnsembleSampler(8, 2, lambda x: -0.5 * np.sum(x ** 2, axis=1), seed=4)
+    with pytest.raises(AttributeError):
+        s.get_chain()
+    st = s.run_mcmc(np.random.default_rng(2).standard_normal((8, 2)), 30)
+    coords, lnp, rstate = st                                  # emcee 3's State unpacking
+    assert isinstance(st, State) and coords.shape == (8, 2) and lnp.shape == (8,)
+    full = s.get_chain()
+    assert full.shape == (30, 8, 2) and s.iteration == 30
+    assert np.array_equal(s.get_chain(discard=5, thin=3), full[5 + 3 - 1::3])       # [discard + thin - 1 :: thin]
+    assert np.array_equal(s.get_chain(flat=True, discard=10), full[10:].reshape(-1, 2))
+    assert np.array_equal(s.get_last_sample().coords, full[-1])
+    assert np.array_equal(coords, full[-1])
+    s.run_mcmc(None, 5)                                       # continues from the last state
+    assert s.get_chain().shape == (35, 8, 2) and np.array_equal(s.get_chain()[:30], full)
+    assert s.get_autocorr_time(tol=0).shape == (2,)
+
+
+def test_walkers_independent():
+    rng = np.random.default_rng(0)
+    assert walkers_independent(rng.standard_normal((16, 4)))
+    x = rng.standard_normal((16, 4))
+    x[:, 2] = 2.0 * x[:, 1]                                   # linearly dependent coordinates
+    assert not walkers_independent(x)
+    x = rng.standard_normal((16, 4))
+    x[:, 0] = 1.0                                             # a constant coordinate
+    assert not walkers_independent(x)
+
+
+def ravest_convergence_loop(sampler, initial_positions, max_steps, interval, start):
+    """ravest's adaptive run_mcmc loop (src/ravest/fit.py:1119-1156), restated: iterate
+    sampler.sample, every `interval` steps after `start` take get_autocorr_time(tol=0) and stop
+    when iteration > 50 tau and tau is stable to 1 %."""
+    history = {}
+    old_tau = np.inf
+    for _sample in sampler.sample(initial_state=initial_positions, iterations=max_steps, progress=False):
+        if sampler.iteration % interval != 0:
+            continue
+        if sampler.iteration < start:
+            continue
+        tau = sampler.get_autocorr_time(tol=0)
+        history[sampler.iteration] = tau.copy()
+        converged = np.all(sampler.iteration > 50 * tau) and np.all(np.abs(old_tau - tau) / tau < 0.01)
+        if converged:
+            break
+        old_tau = tau
+    return history
+
+
+def test_ravest_convergence_loop_stops_early_host():
+    s = EnsembleSampler(32, 2, lambda x: -0.5 * np.sum(x ** 2, axis=1), seed=5)
+    hist = ravest_convergence_loop(s, np.random.default_rng(1).standard_normal((32, 2)), 20000, 250, 500)
+    assert s.iteration < 20000 and s.iteration in hist
+    assert s.get_chain().shape[0] == s.iteration

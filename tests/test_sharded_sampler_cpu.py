@@ -1,0 +1,124 @@
+"""ShardedDeviceSampler's multi-rank orchestration on CPU (gloo, world sizes 2 and 3) with a host
+stand-in for the device operations (tests/_toy_stretch_ops.py): the chain is bitwise the one-rank
+chain, the exchange is the H per-proposal log-probabilities (8 bytes each) per half-step, a NaN in
+one rank's slice makes every rank raise (none hangs in a collective), keep_chain keeps the host
+chain on one rank and the autocorrelation estimate is broadcast from it, and a run stopped early
+and resumed equals an uninterrupted run."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+W, D, STEPS, SPC = 48, 3, 23, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _x0():
+    return np.random.default_rng(5).standard_normal((W, D)) * 0.5
+
+
+def _sampler(nan_at=None, keep="all"):
+    from ravest_amd.distributed import ShardedDeviceSampler
+    from tests._toy_stretch_ops import ToyStretchOps
+    return ShardedDeviceSampler(None, W, seed=11, steps_per_call=SPC, keep_chain=keep, ops=ToyStretchOps(D, nan_at),
+                                device=torch.device("cpu"))
+
+
+def _worker(rank, world, port, q, mode):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        if mode == "chain":
+            s = _sampler()
+            s.run_mcmc(_x0(), STEPS)
+            q.put((rank, s.get_chain(), s.get_log_prob(), s.naccepted.copy(), s.exchange_bytes_per_half_step))
+        elif mode == "nan":
+            s = _sampler(nan_at=(7, 1, W // 2 - 1))          # the last rank's slice
+            try:
+                s.run_mcmc(_x0(), STEPS)
+                q.put((rank, "no error"))
+            except ValueError as e:
+                q.put((rank, str(e), s.iteration))
+        elif mode == "keep":
+            s = _sampler(keep=0)
+            s.run_mcmc(_x0(), STEPS)
+            tau = s.get_autocorr_time(tol=0)
+            try:
+                s.get_chain()
+                has = True
+            except RuntimeError:
+                has = False
+            q.put((rank, has, tau))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_chain_equals_one_rank(world):
+    ref = _sampler()
+    ref.run_mcmc(_x0(), STEPS)
+    for rank, chain, lnp, nacc, xb in _spawn(world, "chain"):
+        assert np.array_equal(chain, ref.get_chain()), rank
+        assert np.array_equal(lnp, ref.get_log_prob()), rank
+        assert np.array_equal(nacc, ref.naccepted), rank
+        assert xb == (W // 2) * 8                          # the exchange: H log-probs per half-step
+    assert ref.naccepted.sum() > 0 and ref.iteration == STEPS
+
+
+def test_nan_raises_on_every_rank():
+    res = _spawn(2, "nan")
+    assert all(r[1] == "Probability function returned NaN" for r in res), res
+    assert all(r[2] == 5 for r in res)                     # the chunk with step 7 starts at step 5
+
+
+def test_keep_chain_on_one_rank_and_broadcast_tau():
+    res = _spawn(2, "keep")
+    assert res[0][1] and not res[1][1]
+    assert np.array_equal(res[0][2], res[1][2]) and np.all(np.isfinite(res[0][2]))
+
+
+def test_early_stop_and_resume_equals_one_run():
+    ref = _sampler()
+    ref.run_mcmc(_x0(), STEPS)
+    s = _sampler()
+    for st in s.sample(_x0(), iterations=STEPS):
+        if s.iteration == 12:                              # inside the third chunk; the fourth is in flight
+            break
+    assert s.iteration == 12
+    assert np.array_equal(s.naccepted, _nacc_at(12))     # exact inside a chunk, generator suspended
+    s.run_mcmc(None, STEPS - 12)
+    assert np.array_equal(s.get_chain(), ref.get_chain())
+    assert np.array_equal(s.get_log_prob(), ref.get_log_prob())
+    assert np.array_equal(s.naccepted, ref.naccepted)
+
+
+def _nacc_at(k):
+    r = _sampler()
+    r.run_mcmc(_x0(), k)
+    return r.naccepted

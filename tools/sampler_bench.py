@@ -65,7 +65,7 @@ def main():
         st = torch.cuda.current_stream(dev)
 
         def run(n, step0, with_chain):
-            _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, 7, step0, 0, 0, 0, 0,
+            _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, 7, step0, 0, 0, 0, 0, 0,
                                          chain.data_ptr() if with_chain else 0, lnpc.data_ptr() if with_chain else 0,
                                          nacc.data_ptr(), status.data_ptr(), st.cuda_stream))
         run(16, 0, True)
