@@ -319,7 +319,7 @@ def config4_sharded_line(world: int, rank: int, backend: str, reps: int = 20) ->
             "bitwise_identical_to_single_gpu": same}
 
 
-def _stretch_raw_ms(lpost, x0, steps: int, warm: int = 16, seed: int = 1234) -> tuple:
+def _stretch_raw_ms(lpost, x0, steps: int, warm: int = 16, seed: int = 1234, flags: int = 0) -> tuple:
     """ms per emcee step of rvk_stretch_run alone (state, draws and chain in HBM, no host copies),
     HIP events on the launch stream; and the acceptance fraction."""
     import torch
@@ -339,7 +339,7 @@ def _stretch_raw_ms(lpost, x0, steps: int, warm: int = 16, seed: int = 1234) -> 
     st = torch.cuda.current_stream(dev)
 
     def run(n, step0):
-        _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, seed, step0, 0, 0, 0, 0, 0,
+        _lib.check(L.rvk_stretch_run(dp._p, x.data_ptr(), lp.data_ptr(), W, n, 2.0, seed, step0, flags, 0, 0, 0, 0,
                                      chain.data_ptr(), lnpc.data_ptr(), nacc.data_ptr(), status.data_ptr(),
                                      st.cuda_stream))
     run(warm, 0)
@@ -380,8 +380,16 @@ def sampler_line(W: int, steps: int = 256, e2e_steps: int = 2048) -> dict:
     t0 = time.perf_counter()
     hs.run_mcmc(x0, 20)
     host_ms = (time.perf_counter() - t0) / 20 * 1e3
+    variants = {}
+    for name, cfg, prior, Wv in (("config2_beta_e", 2, "beta", W), ("config2_vaneylen_e", 2, "vaneylen", W),
+                                 ("config3", 3, "uniform", 16384)):
+        lp_v, x_v = make_posterior(cfg, Wv, device=torch.cuda.current_device(), e_prior=prior)
+        ms_v, acc_v = _stretch_raw_ms(lp_v, x_v, 64 if cfg == 3 else steps)
+        variants[name] = {"walkers": Wv, "free_parameters": x_v.shape[1], "e_prior": prior, "ms_per_step": ms_v,
+                          "walker_steps_per_s": Wv / (ms_v * 1e-3), "acceptance": acc_v}
     return {"what": f"device stretch move (rvk_stretch_run), config-2 posterior, {W} walkers, {D} free parameters, "
                     "Philox draws with emcee 3's randomised split, chain in HBM", "ms_per_step": dev_ms,
+            "posteriors": variants,
             "walker_steps_per_s": W / (dev_ms * 1e-3), "acceptance": acc,
             "run_mcmc_e2e_ms_per_step": e2e_ms, "run_mcmc_e2e_over_kernel": e2e_ms / dev_ms,
             "run_mcmc_e2e_note": f"DeviceEnsembleSampler.run_mcmc of {e2e_steps} steps, call to return, chain + "

@@ -134,12 +134,14 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     constexpr int WB = PassCfg<NP>::WB;
     // SAMPLE & 3: 1 accept / reject of propose_kernel's proposals; 2 proposals made in this kernel
     // + accept / reject; 3 proposals made here, log-posterior out (rvk_stretch_propose).
-    // SAMPLE & 4 (EXT): every prior kind and the prior-side conversion in the fused prep (else the
-    // basic kinds only: no calls, the leaner register budget of the common posterior).
+    // SAMPLE & 4 (ALLP): every prior kind in the fused prep (else the basic kinds only);
+    // SAMPLE & 8 (CONV): + the prior-side conversion (Case 3; an out-of-line call, whose frame
+    // only this variant pays).
     constexpr int MODE = SAMPLE & 3;
     constexpr bool FUSE = MODE >= 2;
     constexpr bool ACCEPT = MODE == 1 || MODE == 2;
-    constexpr bool EXT = (SAMPLE & 4) != 0;
+    constexpr bool CONV = (SAMPLE & 8) != 0;
+    constexpr bool EXT = CONV || (SAMPLE & 4) != 0;
     constexpr int WF = FUSE ? BLK / 64 : 1;   // fused: one walker per wave per pass (launch_sample_fused)
     __shared__ PlanetK pks[WB][NP];
     __shared__ int okp[WB][NP];
@@ -268,8 +270,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     double xv = shfl_d(fv, src < 0 ? 0 : src);
                     if constexpr (EXT) {
                         double d5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-                        if (pd.convert && lane < NP) dead0 |= !to_default_call(pd.par, p5, d5);
-                        if (pd.convert) {                 // wave-uniform branch
+                        if (CONV && lane < NP) dead0 |= !to_default_call(pd.par, p5, d5);
+                        if (CONV) {
                             const int di = src < 0 ? -src - 1 : 0, dp = di / 5, dj = di - 5 * dp;
 #pragma unroll
                             for (int k = 0; k < 5; ++k) {
@@ -786,8 +788,8 @@ loglike_launch_t pick_ll(int np, bool multi, int solver, bool tp) {
 }
 
 // MODE 1: propose_kernel + the likelihood with the accept / reject; 2: one fused half-step;
-// 3: fused proposals, log-posterior out (the fused modes: NP <= 4); | 4: every prior kind and
-// the prior-side conversion in the fused prep.
+// 3: fused proposals, log-posterior out (the fused modes: NP <= 4); | 4: every prior kind;
+// | 8: and the prior-side conversion in the fused prep.
 template <bool MULTI, bool TP, int MODE>
 sample_launch_t pick_sample_s(int np) {
     if constexpr (MODE == 1) {
@@ -955,6 +957,8 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->sample_eval[0] = pick_sample<3>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_fused[1] = pick_sample<6>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_eval[1] = pick_sample<7>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_fused[2] = pick_sample<14>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_eval[2] = pick_sample<15>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;

@@ -1179,8 +1179,7 @@ struct rvk_gp_post {
     double *d_q = nullptr, *d_fac = nullptr, *d_lau = nullptr, *d_nlp = nullptr;
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;
-    PreDraw *d_pre = nullptr;      // [kStepsPerGraph][2][caph] the chunk's draws
-    DrawTable tab;                 // device draws of a block of steps
+    DrawTable tab;                 // the draws of a block of steps
     double *d_xin = nullptr, *d_oin = nullptr;                     // rvk_gp_logpost's staging
     size_t cap_xin = 0, cap_oin = 0;
 
@@ -1207,7 +1206,6 @@ static void free_gp_post(rvk_gp_post *p) {
     (void)hipFree(p->d_nlp);
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
-    (void)hipFree(p->d_pre);
     p->tab.release();
     delete p;
 }
@@ -1220,15 +1218,12 @@ static int gp_post_reserve_half(rvk_gp_post *p, long long H) {
     (void)hipFree(p->d_lau);
     (void)hipFree(p->d_nlp);
     (void)hipFree(p->d_sidx);
-    (void)hipFree(p->d_pre);
     p->d_q = p->d_fac = p->d_lau = p->d_nlp = nullptr;
     p->d_sidx = nullptr;
-    p->d_pre = nullptr;
     p->caph = 0;
     HIPCHK(hipMalloc(&p->d_q, sizeof(double) * (size_t)H * (size_t)p->n_free));
     HIPCHK(hipMalloc(&p->d_fac, sizeof(double) * (size_t)H));
     HIPCHK(hipMalloc(&p->d_lau, sizeof(double) * (size_t)H));
-    HIPCHK(hipMalloc(&p->d_pre, sizeof(PreDraw) * (size_t)kStepsPerGraph * 2 * (size_t)H));
     HIPCHK(hipMalloc(&p->d_nlp, sizeof(double) * (size_t)H));
     HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * (size_t)H));
     if (!p->d_run) HIPCHK(hipMalloc(&p->d_run, sizeof(RunArgs)));
@@ -1382,37 +1377,34 @@ int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t W, int
     const int D = p->n_free;
     const size_t wd = (size_t)W * (size_t)D, hh = 2 * (size_t)H;
     const unsigned blocks = (unsigned)((H + 255) / 256);
-    const int blk = d_set ? n_steps : draws_block_steps(H);
+    const int blk = draws_block_steps(H);
     for (int b0 = 0; b0 < n_steps; b0 += blk) {
         const int nb = (n_steps - b0) < blk ? (n_steps - b0) : blk;
-        if (!d_set && (rc = draws_fill(p->tab, st, H, nb, D, seed, step0 + (uint64_t)b0, a, flags))) return rc;
-        for (int s0 = b0; s0 < b0 + nb; s0 += kStepsPerGraph) {
-            const int n = (b0 + nb - s0) < kStepsPerGraph ? (b0 + nb - s0) : kStepsPerGraph;
-            RunArgs run{d_x,
-                        d_lp,
-                        (long long *)d_naccepted,
-                        (int *)d_status,
-                        d_chain ? d_chain + (size_t)s0 * wd : nullptr,
-                        d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
-                        d_set ? d_set + (size_t)s0 * hh : nullptr,
-                        d_set ? d_zu + (size_t)s0 * hh : nullptr,
-                        d_set ? d_rint + (size_t)s0 * hh : nullptr,
-                        d_set ? d_au + (size_t)s0 * hh : nullptr,
-                        seed,
-                        step0 + (uint64_t)s0,
-                        a};
-            const long long np = (long long)n * 2 * H;
-            hipLaunchKernelGGL(chunk_args_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, p->d_run, run,
-                               p->d_pre, d_set ? nullptr : p->tab.block + (size_t)(s0 - b0) * hh, n, H, D);
-            for (int s = 0; s < n; ++s)
-                for (int half = 0; half < 2; ++half) {
-                    hipLaunchKernelGGL(gp_propose_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, p->d_pre, D, s,
-                                       half, H, p->d_q, p->d_fac, p->d_lau, p->d_sidx);
-                    if ((rc = rvk_gp_logpost_device(p, p->d_q, H, D, p->d_nlp, st))) return rc;
-                    hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, s, H, D,
-                                       p->d_q, p->d_fac, p->d_lau, p->d_sidx, p->d_nlp);
-                }
-        }
+        const RunArgs run{d_x,
+                          d_lp,
+                          (long long *)d_naccepted,
+                          (int *)d_status,
+                          d_chain ? d_chain + (size_t)b0 * wd : nullptr,
+                          d_lnp ? d_lnp + (size_t)b0 * (size_t)W : nullptr,
+                          d_set ? d_set + (size_t)b0 * hh : nullptr,
+                          d_set ? d_zu + (size_t)b0 * hh : nullptr,
+                          d_set ? d_rint + (size_t)b0 * hh : nullptr,
+                          d_set ? d_au + (size_t)b0 * hh : nullptr,
+                          seed,
+                          step0 + (uint64_t)b0,
+                          a};
+        rc = d_set ? draws_fill_host(p->tab, st, H, nb, D, run)
+                   : draws_fill(p->tab, st, H, nb, D, seed, step0 + (uint64_t)b0, a, flags);
+        if (rc) return rc;
+        hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+        for (int s = 0; s < nb; ++s)
+            for (int half = 0; half < 2; ++half) {
+                hipLaunchKernelGGL(gp_propose_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, p->tab.block, D, s,
+                                   half, H, p->d_q, p->d_fac, p->d_lau, p->d_sidx);
+                if ((rc = rvk_gp_logpost_device(p, p->d_q, H, D, p->d_nlp, st))) return rc;
+                hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, s, H, D, p->d_q,
+                                   p->d_fac, p->d_lau, p->d_sidx, p->d_nlp);
+            }
     }
     HIPCHK(hipGetLastError());
     return RVK_OK;

@@ -54,7 +54,7 @@ int grow_dev(void **p, size_t *cap, size_t need);
 // Per-device copy of the sin/cos table, uploaded once per process (never freed).
 int shared_table(int device, const SC **tab);
 
-// Steps per cached graph replay of the device stretch move (and per chunk_args_kernel).
+// Draw blocks (and the device stretch move's cached graphs) are a multiple of this many steps.
 constexpr int kStepsPerGraph = 8;
 
 // The stretch move's device draws (split_draws_kernel) for a block of steps: table[s][half][j]
@@ -69,9 +69,11 @@ struct DrawTable {
     void release();
 };
 
-// Fill `t` with the draws of n_steps steps from global step step0 (RVK_STRETCH_* flags), stream-ordered.
+// Fill `t` with the draws of n_steps steps from global step step0 (RVK_STRETCH_* flags), stream-ordered;
+// with host draws (run.set != NULL) from those instead.
 int draws_fill(DrawTable &t, hipStream_t st, long long H, int n_steps, int D, uint64_t seed, uint64_t step0, double a,
                int flags);
+int draws_fill_host(DrawTable &t, hipStream_t st, long long H, int n_steps, int D, const RunArgs &run);
 // Steps per draw block for H walkers per half: a multiple of kStepsPerGraph, table <= 256 MB.
 int draws_block_steps(long long H);
 
@@ -110,9 +112,9 @@ struct rvk_handle {
     rvk::loglike_launch_t launch = nullptr;
     rvk::sample_launch_t sample = nullptr;   // fused stretch-move half-step (production solver)
     // ... with the proposals made in the same kernel, and proposals + log-posterior only
-    // (rvk_stretch_propose); [1]: every prior kind and the prior-side conversion in the prep
-    rvk::sample_launch_t sample_fused[2] = {nullptr, nullptr};
-    rvk::sample_launch_t sample_eval[2] = {nullptr, nullptr};
+    // (rvk_stretch_propose); [1]: every prior kind, [2]: + the prior-side conversion in the prep
+    rvk::sample_launch_t sample_fused[3] = {nullptr, nullptr, nullptr};
+    rvk::sample_launch_t sample_eval[3] = {nullptr, nullptr, nullptr};
     int solver = 0;
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW

@@ -89,7 +89,7 @@ struct rvk_post {
     int n_free = 0, n_prior = 0;
     bool convert = false;
     bool fusable = false;                  // proposals can be made inside the likelihood kernel
-    int ext = 0;                           // ... with a transcendental prior kind or the conversion
+    int ext = 0;                           // ... 1: with a transcendental prior kind, 2: + the conversion
     double jac = 0.0, renorm = 0.0;
     int32_t *d_colmap = nullptr;
     double *d_tmpl = nullptr;
@@ -99,14 +99,13 @@ struct rvk_post {
     double *d_full = nullptr, *d_lp = nullptr, *d_q = nullptr, *d_fac = nullptr, *d_nlp = nullptr, *d_lau = nullptr;
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;              // rvk_stretch_run's per-chunk arguments
-    PreDraw *d_pre = nullptr;              // [kStepsPerGraph][2][caph] the chunk's draws (fixed address)
-    long long caph = 0;
-    DrawTable tab;                         // device draws of a block of steps (split_draws_kernel)
+    DrawTable tab;                         // the draws of a block of steps (split_draws_kernel / host draws)
     double *d_xin = nullptr, *d_oin = nullptr;   // rvk_logpost's host-buffer staging, grown on demand
     size_t cap_xin = 0, cap_oin = 0;
     hipStream_t cap = nullptr;             // capture stream
-    hipGraphExec_t graph = nullptr;        // cached kStepsPerGraph-step chunk
+    hipGraphExec_t graph = nullptr;        // cached block of steps (draws_block_steps(H) steps)
     long long graph_H = 0;
+    const PreDraw *graph_tab = nullptr;    // the draw table the graph reads
     int graph_solver = -1;
 
     PostDev dev() const {
@@ -145,22 +144,23 @@ static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long
     }
 }
 
-// Kernels of n steps (both halves, all proposals) reading this chunk's RunArgs and draws.
+// Kernels of n steps (both halves, all proposals) reading the block's RunArgs and draw table.
 static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
     for (int s = 0; s < n; ++s)
-        for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H, p->d_pre);
+        for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H, p->tab.block);
 }
 
-// The kStepsPerGraph-step chunk as a HIP graph, captured once per (H, solver) and
-// replayed: its kernel arguments never change (everything per call is in d_run).
-static int ensure_graph(rvk_post *p, long long H) {
-    if (p->graph && p->graph_H == H && p->graph_solver == p->h->solver) return RVK_OK;
+// A whole block of steps (2 x draws_block_steps(H) half-step kernels) as one HIP graph, captured
+// once per (H, solver, draw table) and replayed: its kernel arguments never change (everything
+// per call is in d_run and the draw table), so a block is one launch.
+static int ensure_graph(rvk_post *p, long long H, int steps) {
+    if (p->graph && p->graph_H == H && p->graph_solver == p->h->solver && p->graph_tab == p->tab.block) return RVK_OK;
     if (p->graph) (void)hipGraphExecDestroy(p->graph);
     p->graph = nullptr;
     if (!p->cap) HIPCHK(hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking));
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(p->cap, hipStreamCaptureModeRelaxed));
-    enqueue_steps(p, p->cap, H, kStepsPerGraph);
+    enqueue_steps(p, p->cap, H, steps);
     HIPCHK(hipStreamEndCapture(p->cap, &g));
     const hipError_t e = hipGraphInstantiate(&p->graph, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
@@ -170,6 +170,7 @@ static int ensure_graph(rvk_post *p, long long H) {
     }
     p->graph_H = H;
     p->graph_solver = p->h->solver;
+    p->graph_tab = p->tab.block;
     return RVK_OK;
 }
 
@@ -187,7 +188,6 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_lau);
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
-    (void)hipFree(p->d_pre);
     p->tab.release();
     (void)hipFree(p->d_xin);
     (void)hipFree(p->d_oin);
@@ -220,20 +220,6 @@ static int reserve_impl(rvk_post *p, long long W) {
     HIPCHK(hipMalloc(&p->d_lau, sizeof(double) * w));
     HIPCHK(hipMalloc(&p->d_sidx, sizeof(long long) * w));
     p->capw = W;
-    return RVK_OK;
-}
-
-// The chunk's draw region for H walkers per half (the graph reads it at a fixed address).
-static int reserve_chunk(rvk_post *p, long long H) {
-    if (H <= p->caph) return RVK_OK;
-    if (p->graph) (void)hipGraphExecDestroy(p->graph);
-    p->graph = nullptr;
-    HIPCHK(hipSetDevice(p->h->device));
-    (void)hipFree(p->d_pre);
-    p->d_pre = nullptr;
-    p->caph = 0;
-    HIPCHK(hipMalloc(&p->d_pre, sizeof(PreDraw) * (size_t)kStepsPerGraph * 2 * (size_t)H));
-    p->caph = H;
     return RVK_OK;
 }
 
@@ -274,7 +260,7 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
     p->fusable = n_free <= kFuseMaxD && pf <= kFuseMaxPFull && n_prior <= kFuseMaxPrior && !(fe && atoi(fe) == 0);
     bool basic = true;
     for (int k = 0; k < n_prior; ++k) basic &= kind[k] <= kMaxBasicPriorKind;
-    p->ext = (basic && !convert) ? 0 : 1;
+    p->ext = convert ? 2 : basic ? 0 : 1;
     p->jac = jac;
     p->renorm = renorm;
     HIPCHK(hipSetDevice(h->device));
@@ -309,11 +295,31 @@ int rvk::draws_block_steps(long long H) {
     return (int)(n < kStepsPerGraph ? kStepsPerGraph : n);
 }
 
+// Room for a block of draws: at least draws_block_steps(H) steps, so the table (and a graph reading
+// it) keeps its address from one block to the next.
+static int draws_reserve(DrawTable &t, long long H, int n_steps) {
+    const int blk = draws_block_steps(H);
+    const size_t n = (size_t)(n_steps > blk ? n_steps : blk);
+    return grow_dev((void **)&t.block, &t.cap_block, sizeof(PreDraw) * 2 * (size_t)H * n);
+}
+
+int rvk::draws_fill_host(DrawTable &t, hipStream_t st, long long H, int n_steps, int D, const RunArgs &run) {
+    int rc = draws_reserve(t, H, n_steps);
+    if (rc) return rc;
+    const long long np = (long long)n_steps * 2 * H;
+    hipLaunchKernelGGL(host_draws_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, t.block, run, n_steps,
+                       H, D);
+    HIPCHK(hipGetLastError());
+    t.H = H;
+    t.steps = n_steps;
+    return RVK_OK;
+}
+
 int rvk::draws_fill(DrawTable &t, hipStream_t st, long long H, int n_steps, int D, uint64_t seed, uint64_t step0,
                     double a, int flags) {
     const size_t W = 2 * (size_t)H, n = (size_t)n_steps;
     int rc;
-    if ((rc = grow_dev((void **)&t.block, &t.cap_block, sizeof(PreDraw) * W * n)) ||
+    if ((rc = draws_reserve(t, H, n_steps)) ||
         (rc = grow_dev((void **)&t.keys, &t.cap_keys, sizeof(uint32_t) * W * n)) ||
         (rc = grow_dev((void **)&t.sets, &t.cap_sets, sizeof(int32_t) * W * n)))
         return rc;
@@ -402,7 +408,7 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
     if (n_steps == 0) return RVK_OK;
     const long long H = W / 2;
     int rc = reserve_impl(p, H);
-    if (rc || (rc = reserve_chunk(p, H))) return rc;
+    if (rc) return rc;
     rvk_handle *h = p->h;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
@@ -410,34 +416,31 @@ int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n
     HIPCHK(hipStreamIsCapturing(st, &cs));
     const bool use_graph = h->graph && cs == hipStreamCaptureStatusNone;   // a caller's capture records the launches
     const size_t wd = (size_t)W * (size_t)p->n_free, hh = 2 * (size_t)H;
-    const int blk = d_set ? n_steps : draws_block_steps(H);               // steps per device draw block
+    const int blk = draws_block_steps(H);                                 // steps per draw block (and graph)
     for (int b0 = 0; b0 < n_steps; b0 += blk) {
         const int nb = (n_steps - b0) < blk ? (n_steps - b0) : blk;
-        if (!d_set && (rc = draws_fill(p->tab, st, H, nb, p->n_free, seed, step0 + (uint64_t)b0, a, flags))) return rc;
-        for (int s0 = b0; s0 < b0 + nb; s0 += kStepsPerGraph) {
-            const int n = (b0 + nb - s0) < kStepsPerGraph ? (b0 + nb - s0) : kStepsPerGraph;
-            RunArgs run{d_x,
-                        d_lp,
-                        (long long *)d_naccepted,
-                        (int *)d_status,
-                        d_chain ? d_chain + (size_t)s0 * wd : nullptr,
-                        d_lnp ? d_lnp + (size_t)s0 * (size_t)W : nullptr,
-                        d_set ? d_set + (size_t)s0 * hh : nullptr,
-                        d_set ? d_zu + (size_t)s0 * hh : nullptr,
-                        d_set ? d_rint + (size_t)s0 * hh : nullptr,
-                        d_set ? d_au + (size_t)s0 * hh : nullptr,
-                        seed,
-                        step0 + (uint64_t)s0,
-                        a};
-            const long long np = (long long)n * 2 * H;
-            hipLaunchKernelGGL(chunk_args_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, p->d_run, run,
-                               p->d_pre, d_set ? nullptr : p->tab.block + (size_t)(s0 - b0) * hh, n, H, p->n_free);
-            if (use_graph && n == kStepsPerGraph) {
-                if ((rc = ensure_graph(p, H))) return rc;
-                HIPCHK(hipGraphLaunch(p->graph, st));
-            } else {
-                enqueue_steps(p, st, H, n);
-            }
+        const RunArgs run{d_x,
+                          d_lp,
+                          (long long *)d_naccepted,
+                          (int *)d_status,
+                          d_chain ? d_chain + (size_t)b0 * wd : nullptr,
+                          d_lnp ? d_lnp + (size_t)b0 * (size_t)W : nullptr,
+                          d_set ? d_set + (size_t)b0 * hh : nullptr,
+                          d_set ? d_zu + (size_t)b0 * hh : nullptr,
+                          d_set ? d_rint + (size_t)b0 * hh : nullptr,
+                          d_set ? d_au + (size_t)b0 * hh : nullptr,
+                          seed,
+                          step0 + (uint64_t)b0,
+                          a};
+        rc = d_set ? draws_fill_host(p->tab, st, H, nb, p->n_free, run)
+                   : draws_fill(p->tab, st, H, nb, p->n_free, seed, step0 + (uint64_t)b0, a, flags);
+        if (rc) return rc;
+        hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+        if (use_graph && nb == blk) {
+            if ((rc = ensure_graph(p, H, blk))) return rc;
+            HIPCHK(hipGraphLaunch(p->graph, st));
+        } else {
+            enqueue_steps(p, st, H, nb);
         }
     }
     HIPCHK(hipGetLastError());

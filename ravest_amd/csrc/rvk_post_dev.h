@@ -67,9 +67,8 @@ __device__ __forceinline__ double prior_lp_basic(int kind, const double *p, doub
     }
 }
 
-// The prior kinds with a transcendental function (Rayleigh, VanEylen19Mixture, Beta), out of
-// line: their log / log1p / exp cost registers only while they run.
-__device__ __attribute__((noinline)) double prior_lp_trans(int kind, const double *p, double x) {
+// The prior kinds with a transcendental function (Rayleigh, VanEylen19Mixture, Beta).
+__device__ __forceinline__ double prior_lp_trans(int kind, const double *p, double x) {
     switch (kind) {
         case RVK_PRIOR_RAYLEIGH:
             if (x < 0.0) return -INFINITY;
@@ -485,21 +484,14 @@ static __global__ __launch_bounds__(256) void stretch_update_kernel(const PreDra
 
 static __global__ void set_run_kernel(RunArgs *dst, RunArgs v) { *dst = v; }
 
-// The chunk's arguments plus every proposal's draws of its n steps (one thread per proposal) at
-// the chunk's fixed address `pre` (so a cached graph of the chunk reads them): a copy of the
-// device draws (`src`, split_draws_kernel) or, with host draws (v.set), the PreDraw of each.
-static __global__ __launch_bounds__(256) void chunk_args_kernel(RunArgs *dst, RunArgs v, PreDraw *__restrict__ pre,
-                                                                const PreDraw *__restrict__ src, int n, long long H,
-                                                                int D) {
+// Host-supplied draws (emcee's RandomState stream, RunArgs v.set / zu / rint / au for the block's
+// n steps) into the draw table the sampler kernels read: one thread per proposal.
+static __global__ __launch_bounds__(256) void host_draws_kernel(PreDraw *__restrict__ tab, RunArgs v, int n,
+                                                                long long H, int D) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *dst = v;
     if (i >= (long long)n * 2 * H) return;
-    if (src) {
-        pre[i] = src[i];
-    } else {
-        const long long sh = i / H;
-        pre[i] = make_pre_host(v, (int)(sh >> 1), (int)(sh & 1), i - sh * H, H, D);
-    }
+    const long long sh = i / H;
+    tab[i] = make_pre_host(v, (int)(sh >> 1), (int)(sh & 1), i - sh * H, H, D);
 }
 
 

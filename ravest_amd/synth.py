@@ -154,9 +154,13 @@ def make_config(cfg: int, n_walkers: int | None = None) -> Dataset:
     return ds
 
 
-def make_posterior(config: int = 2, n_walkers: int | None = None, device: int = -1, seed: int = 0):
+def make_posterior(config: int = 2, n_walkers: int | None = None, device: int = -1, seed: int = 0,
+                   e_prior: str = "uniform"):
     """A LogPosterior over the config's synthetic dataset with built-in priors on every
     free parameter (trend fixed at 0), and a tight starting ball around the truth.
+    ``e_prior``: the eccentricity prior -- "uniform" (EccentricityUniform(0.99)), or one of
+    ravest's eccentricity priors "beta" (Kipping 2013's Beta(0.867, 3.03)), "rayleigh"
+    (Rayleigh(0.2)), "vaneylen" (VanEylen19Mixture(0.049, 0.26, 0.08)) (prior.py:252-511).
     Used by the sampler benchmarks (bench.py "sampler", tools/sampler_bench.py)."""
     from . import prior as P
     from .posterior import LogPosterior
@@ -168,7 +172,9 @@ def make_posterior(config: int = 2, n_walkers: int | None = None, device: int = 
         v = ds.truth[n]
         base = n.split("_")[0]
         if base == "e":
-            priors[n] = P.EccentricityUniform(0.99)
+            priors[n] = {"uniform": lambda: P.EccentricityUniform(0.99), "beta": lambda: P.Beta(0.867, 3.03),
+                         "rayleigh": lambda: P.Rayleigh(0.2),
+                         "vaneylen": lambda: P.VanEylen19Mixture(0.049, 0.26, 0.08)}[e_prior]()
         elif base == "w":
             priors[n] = P.Uniform(-np.pi, np.pi)
         elif base == "jit":

@@ -125,20 +125,37 @@ def test_device_posterior_from_foreign_objects(name):
     assert_ll_close(lpost.log_probability_batch(case["theta_free"]), case["log_prob"], what=f"foreign-host-{name}")
 
 
-@pytest.mark.parametrize("rng", ["philox", "emcee"])
-def test_fused_sampler_equals_two_kernel_path(monkeypatch, rng):
-    """The fused half-step (proposals made in the likelihood kernel's prep, basic prior kinds)
-    gives the same chain, log-probs and acceptances, bit for bit, as propose_kernel + the
-    likelihood kernel (RVK_SAMPLER_FUSE=0)."""
+def _fused_case(what, W):
+    """Posteriors for the fused half-step: config 2 with every eccentricity prior kind (basic and
+    transcendental), config 3 (3 planets, 2 instruments, D = 19), and the reference's Case-3
+    posterior (Beta priors on e converted from secosw / sesinw, 2 planets, 2 instruments)."""
     from ravest_amd.synth import make_posterior
+    if what == "case3":
+        return _start(load_case("case3"), W, 13)
+    cfg, prior = {"cfg2": (2, "uniform"), "cfg2_beta": (2, "beta"), "cfg2_rayleigh": (2, "rayleigh"),
+                  "cfg2_vaneylen": (2, "vaneylen"), "cfg3": (3, "uniform")}[what]
+    return make_posterior(cfg, W, seed=4, e_prior=prior)
+
+
+@pytest.mark.parametrize("what,rng", [("cfg2", "philox"), ("cfg2", "emcee"), ("cfg2_beta", "philox"),
+                                      ("cfg2_rayleigh", "philox"), ("cfg2_vaneylen", "emcee"), ("cfg3", "philox"),
+                                      ("case3", "philox"), ("case3", "emcee")])
+def test_fused_sampler_equals_two_kernel_path(monkeypatch, what, rng):
+    """The fused half-step (proposals, full row, conversion and priors made lane-parallel in the
+    likelihood kernel's prep) gives the same chain, log-probs and acceptances, bit for bit, as
+    propose_kernel + the likelihood kernel (RVK_SAMPLER_FUSE=0): basic and transcendental prior
+    kinds, D up to 19, the prior-side conversion."""
+    W = 64 if what == "case3" else 256
     runs = []
     for fuse in ("1", "0"):
         monkeypatch.setenv("RVK_SAMPLER_FUSE", fuse)
-        lpost, x0 = make_posterior(2, 256, seed=4)
+        lpost, x0 = _fused_case(what, W)
         seed = np.random.RandomState(21) if rng == "emcee" else 99
-        s = DeviceEnsembleSampler(lpost, 256, seed=seed, rng=rng, steps_per_call=8)
-        s.run_mcmc(x0, 24)
+        s = DeviceEnsembleSampler(lpost, W, seed=seed, rng=rng, steps_per_call=8)
+        s.run_mcmc(x0, 24, skip_initial_state_check=(what == "case3"))
         runs.append((s.get_chain(), s.get_log_prob(), s.naccepted.copy()))
     (c1, l1, a1), (c0, l0, a0) = runs
     assert np.array_equal(c1, c0) and np.array_equal(l1, l0) and np.array_equal(a1, a0)
     assert a1.sum() > 0
+    lpost, _ = _fused_case(what, W)
+    assert_ll_close(l1[-1], lpost.log_probability_batch(c1[-1]), what=f"fused-{what}-last-step")
