@@ -137,6 +137,11 @@ int rvk_stretch_draws(rvk_post *p, int64_t n_walkers, int32_t n_steps, double a,
                       int32_t flags, void *stream);
 int rvk_stretch_propose(rvk_post *p, const double *d_x, int64_t n_walkers, int32_t s, int32_t half, int64_t j0,
                         int64_t count, double *d_out, void *stream);
+/* Copy `bytes` (a multiple of 16, 16-byte aligned) from device memory to pinned host memory
+ * with `workgroups` workgroups (1..1024), stream-ordered: how the samplers stream each finished
+ * chunk of the chain out over PCIe beside the running chunk without a full-grid copy kernel. */
+int rvk_copy_to_host(const void *d_src, void *h_dst, int64_t bytes, int32_t workgroups, void *stream);
+
 /* Diagnostics: the drawn table's (walker, complement, z) of the W/2 proposals of (s, half), into
  * host buffers (blocking; synchronises the device). */
 int rvk_stretch_table_read(rvk_post *p, int32_t s, int32_t half, int64_t *walker, int64_t *complement, double *z);

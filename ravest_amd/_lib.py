@@ -20,7 +20,7 @@ EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rv
            "rvk_solve_kepler", "rvk_set_option", "rvk_stream", "rvk_sync", "rvk_device_count",
            "rvk_last_error", "rvk_version",
            "rvk_post_create", "rvk_post_destroy", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
-           "rvk_stretch_run", "rvk_stretch_draws", "rvk_stretch_propose", "rvk_stretch_update", "rvk_stretch_table_read",
+           "rvk_stretch_run", "rvk_stretch_draws", "rvk_stretch_propose", "rvk_stretch_update", "rvk_stretch_table_read", "rvk_copy_to_host",
            "rvk_gp_create", "rvk_gp_destroy", "rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_gp_set_precision",
            "rvk_gp_predict", "rvk_gp_predict_device", "rvk_gp_post_create", "rvk_gp_post_destroy",
            "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device", "rvk_gp_stretch_run"]
@@ -101,6 +101,7 @@ def load() -> C.CDLL:
     L.rvk_stretch_draws.argtypes = [vp, C.c_int64, C.c_int32, C.c_double, C.c_uint64, C.c_uint64, C.c_int32, vp]
     L.rvk_stretch_propose.argtypes = [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int64, vp, vp]
     L.rvk_stretch_table_read.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]
+    L.rvk_copy_to_host.argtypes = [vp, vp, C.c_int64, C.c_int32, vp]
     L.rvk_stretch_update.argtypes = [vp, vp, vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp]
     L.rvk_gp_create.argtypes = [vp, C.c_int32]
     L.rvk_gp_create.restype = vp
@@ -125,7 +126,7 @@ def load() -> C.CDLL:
                  "rvk_gp_stretch_run", "rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
                  "rvk_set_option", "rvk_reserve", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
                  "rvk_stretch_run", "rvk_stretch_draws", "rvk_stretch_propose", "rvk_stretch_update",
-                 "rvk_stretch_table_read"):
+                 "rvk_stretch_table_read", "rvk_copy_to_host"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L

@@ -74,6 +74,16 @@ __global__ __launch_bounds__(256) void propose_kernel(PostDev pd, const RunArgs 
     }
 }
 
+// Device -> pinned host memory with a few workgroups (rvk_copy_to_host): a sampler chunk's chain
+// streams out over PCIe on a handful of CUs beside the sampler's kernels, instead of a full-grid
+// blit kernel competing with them for every CU.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void egress_kernel(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst,
+                                                     long long n16) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256)
+        dst[i] = __builtin_nontemporal_load(src + i);
+}
+
 unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
 
 // one wave per item, at most 2^16 blocks (grid-stride beyond)
@@ -487,6 +497,19 @@ int rvk_stretch_propose(rvk_post *p, const double *d_x, int64_t W, int32_t s, in
                            half, count, j0, H, p->d_q, p->d_full, p->d_lp, p->d_fac, p->d_lau, p->d_sidx);
         h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, count, h->p_full(), d_out, post);
     }
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_copy_to_host(const void *d_src, void *h_dst, int64_t bytes, int32_t workgroups, void *stream) {
+    if (bytes < 0 || (bytes > 0 && (!d_src || !h_dst))) return fail(RVK_E_ARG, "bad copy arguments");
+    if (bytes == 0) return RVK_OK;
+    if (((uintptr_t)d_src | (uintptr_t)h_dst | (uintptr_t)bytes) & 15u)
+        return fail(RVK_E_ARG, "rvk_copy_to_host needs 16-byte aligned pointers and size");
+    if (workgroups < 1) workgroups = 1;
+    if (workgroups > 1024) workgroups = 1024;
+    hipLaunchKernelGGL(egress_kernel, dim3((unsigned)workgroups), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)d_src, (u32x4 *)h_dst, (long long)(bytes / 16));
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 
 import numpy as np
 
@@ -188,6 +189,28 @@ def emcee_step_draws(random: np.random.RandomState, nwalkers: int):
     return sets, zu, rint, au
 
 
+def _host_array(shape) -> np.ndarray:
+    """An fp64 host array for a chain: large ones on an anonymous mapping advised for transparent
+    huge pages, so the first touch (the chunk copy-out) faults 2 MB pages, not 4 KB ones (a 58 MB
+    chunk lands in ~0.5 ms instead of ~4 ms on the GPU box)."""
+    n = int(np.prod(shape))
+    if n * 8 < (2 << 20):
+        return np.empty(shape)
+    import mmap
+    m = mmap.mmap(-1, n * 8, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    try:
+        m.madvise(mmap.MADV_HUGEPAGE)
+    except (AttributeError, OSError):
+        pass
+    return np.frombuffer(m, dtype=np.float64, count=n).reshape(shape)
+
+
+def _copy(dst: np.ndarray, src) -> None:
+    """dst[...] = src with torch's multi-threaded copy (src: a host tensor or array)."""
+    import torch
+    torch.from_numpy(dst).copy_(src if isinstance(src, torch.Tensor) else torch.from_numpy(np.asarray(src)))
+
+
 def _random_state(seed):
     if isinstance(seed, np.random.RandomState):
         return seed
@@ -212,10 +235,11 @@ class _Backend:
         need = self.iteration + ngrow
         if need <= len(self.chain):
             return
-        chain = np.empty((need, self.nwalkers, self.ndim))       # untouched pages cost nothing
-        lnp = np.empty((need, self.nwalkers))
-        chain[:self.iteration] = self.chain[:self.iteration]
-        lnp[:self.iteration] = self.log_prob[:self.iteration]
+        chain = _host_array((need, self.nwalkers, self.ndim))    # untouched pages cost nothing
+        lnp = _host_array((need, self.nwalkers))
+        if self.iteration:
+            _copy(chain[:self.iteration], self.chain[:self.iteration])
+            _copy(lnp[:self.iteration], self.log_prob[:self.iteration])
         self.chain, self.log_prob = chain, lnp
 
     def get_value(self, name: str, flat=False, thin=1, discard=0):
@@ -420,6 +444,7 @@ class _DevicePipeline(_SamplerBase):
         self._copy_stream = None
         self._nslot = 0
         self._accepted_iter = 0              # backend.accepted is exact at this iteration
+        self._trace = [] if os.environ.get("RVK_SAMPLER_TRACE") else None   # (phase, perf_counter) timing probe
 
     @property
     def _cuda(self) -> bool:
@@ -442,7 +467,7 @@ class _DevicePipeline(_SamplerBase):
                                  torch.empty((n, W), dtype=torch.float64, **pin) if self._keep_host else None,
                                  torch.empty(1, dtype=torch.int32, **pin))
             if self._copy_stream is None:
-                self._copy_stream = torch.cuda.Stream(self.device)
+                self._copy_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("RVK_COPY_PRIO", "0")))
         else:                                 # host tensors: the device buffers are the staging
             self._stage[slot] = (self._dbuf[slot][0], self._dbuf[slot][1], self._status)
 
@@ -479,18 +504,30 @@ class _DevicePipeline(_SamplerBase):
             stream.wait_event(prev.copied)    # the slot's device buffers were being copied out
         ch = _Chunk()
         ch.start, ch.n, ch.slot, ch.copied = self._dev_iter, n, slot, None
+        if self._trace is not None:
+            self._trace.append(("enqueue", time.perf_counter()))
         self._begin_chunk(ch)
         chain_d, lnp_d = self._dbuf[slot]
         self._run_chunk(ch, chain_d, lnp_d, stream)
+        if self._trace is not None:
+            self._trace.append(("launched", time.perf_counter()))
         self._dev_iter += n
         if self._cuda:
             computed = torch.cuda.Event()
             computed.record(stream)
             cs = self._copy_stream
             cs.wait_event(computed)
+            sc, sl, ss = self._stage[slot]
+            wg = int(os.environ.get("RVK_EGRESS_WG", "0"))   # experiment hook: copy with a few workgroups
+            if self._keep_host and wg:
+                from . import _lib
+                L = _lib.load()
+                _lib.check(L.rvk_copy_to_host(chain_d.data_ptr(), sc.data_ptr(), n * chain_d[0].numel() * 8, wg,
+                                              cs.cuda_stream))
+                _lib.check(L.rvk_copy_to_host(lnp_d.data_ptr(), sl.data_ptr(), n * lnp_d[0].numel() * 8, wg,
+                                              cs.cuda_stream))
             with torch.cuda.stream(cs):
-                sc, sl, ss = self._stage[slot]
-                if self._keep_host:
+                if self._keep_host and not wg:
                     sc[:n].copy_(chain_d[:n], non_blocking=True)
                     sl[:n].copy_(lnp_d[:n], non_blocking=True)
                 ss.copy_(self._status, non_blocking=True)
@@ -501,10 +538,17 @@ class _DevicePipeline(_SamplerBase):
         self._chunks = (self._chunks + [ch])[-3:]
         return ch
 
+    def run_mcmc(self, initial_state, nsteps: int, **kwargs):
+        """emcee's run_mcmc (iterates sample, returns the last State), without a Python object per step."""
+        results = None
+        for results in self.sample(initial_state, iterations=nsteps, _per_step=False, **kwargs):
+            pass
+        return results
+
     def sample(self, initial_state=None, log_prob0=None, rstate0=None, blobs0=None, iterations=1, tune=False,
-               skip_initial_state_check=False, thin_by=1, thin=None, store=True, progress=False, progress_kwargs=None):
+               skip_initial_state_check=False, thin_by=1, thin=None, store=True, progress=False, progress_kwargs=None,
+               _per_step=True):
         """emcee's EnsembleSampler.sample: yields a State per step (``iteration`` counts them)."""
-        import torch
         self._unsupported(thin_by, thin, blobs0)
         self._settle()
         self._token += 1
@@ -530,6 +574,8 @@ class _DevicePipeline(_SamplerBase):
             if pending is not None:
                 if pending.copied is not None:
                     pending.copied.synchronize()
+                if self._trace is not None:
+                    self._trace.append(("copied", time.perf_counter()))
                 sc, sl, ss = self._stage[pending.slot]
                 if int(ss[0]):
                     self._status.zero_()
@@ -537,8 +583,23 @@ class _DevicePipeline(_SamplerBase):
                 b = self.backend
                 a, e = pending.start, pending.start + pending.n
                 if store:                     # multi-threaded copy out of the pinned staging
-                    torch.from_numpy(b.chain[a:e]).copy_(sc[:pending.n])
-                    torch.from_numpy(b.log_prob[a:e]).copy_(sl[:pending.n])
+                    _copy(b.chain[a:e], sc[:pending.n])
+                    _copy(b.log_prob[a:e], sl[:pending.n])
+                if self._trace is not None:
+                    self._trace.append(("stored", time.perf_counter()))
+                if not _per_step:             # run_mcmc: the chunk's last state only
+                    if tok != self._token:
+                        raise RuntimeError("this run was superseded by a later sample()/run_mcmc()/reset() call")
+                    b.iteration = e
+                    if bar is not None:
+                        bar.update(pending.n)
+                    yield (State(b.chain[e - 1], log_prob=b.log_prob[e - 1]) if store else
+                           State(sc[pending.n - 1].numpy(), log_prob=sl[pending.n - 1].numpy(), copy=True)
+                           if sc is not None else State(np.empty((0, self.ndim))))
+                    if nxt is None:
+                        break
+                    pending = nxt
+                    continue
                 for i in range(pending.n):
                     if tok != self._token:
                         raise RuntimeError("this sample() generator was superseded by a later sample()/run_mcmc()/"
