@@ -42,8 +42,11 @@ extern "C" {
 #define RVK_PAR_PKSECOSWSESINWTP  2   /* "P K secosw sesinw Tp" */
 #define RVK_PAR_PKSECOSWSESINWTC  3   /* "P K secosw sesinw Tc" */
 
-#define RVK_MAX_PLANETS 8
-#define RVK_MAX_INST    16
+/* Limits of one handle.  Up to 8 planets run kernels specialised on the planet count; 9 to
+ * RVK_MAX_PLANETS run one generic kernel (planet constants in LDS).  Instruments are a runtime
+ * loop. */
+#define RVK_MAX_PLANETS 32
+#define RVK_MAX_INST    64
 
 /* error codes */
 #define RVK_OK          0
@@ -53,9 +56,11 @@ extern "C" {
 #define RVK_E_NOMEM    -4
 
 /* rvk_predict component mask */
-#define RVK_PRED_PLANETS  0x00FFu  /* bit p: include planet p */
+#define RVK_PRED_PLANETS  0x00FFu  /* bit p: include planet p (p < 8) */
 #define RVK_PRED_TREND    0x0100u  /* include gd*(t-t0) + gdd*(t-t0)^2 */
 #define RVK_PRED_GAMMA    0x0200u  /* include g[inst] (needs inst per time) */
+#define RVK_PRED_ALL_PLANETS 0x0400u  /* include every planet (any count) */
+#define RVK_PRED_PLANET(p) (0x0800u | ((uint32_t)(p) << 16))   /* include planet p (any p) */
 
 typedef struct rvk_handle rvk_handle;
 

@@ -31,6 +31,13 @@ OPT_LPW = 3
 
 PRED_TREND = 0x0100
 PRED_GAMMA = 0x0200
+PRED_ALL_PLANETS = 0x0400
+MAX_PLANETS, MAX_INST = 32, 64
+
+
+def pred_planet(p: int) -> int:
+    """RVK_PRED_PLANET(p): include planet p (any index)."""
+    return 0x0800 | (int(p) << 16)
 
 # include/rvk_post.h
 PRIOR_NPAR = 8

@@ -121,9 +121,12 @@ __device__ unsigned long long g_ll_trace[16][8];
 // of propose_kernel + this one, and no block barrier separates a walker's prep from its loop.
 // Same arithmetic and order as propose_kernel / post_row_wave (rvk_post.hip,
 // rvk_post_dev.h), so the chain is the same bit for bit.
+// NP = 0: the generic kernel, planet count d.np (9 .. RVK_MAX_PLANETS), one walker per wave per pass
+// and its planet constants read from LDS in the epoch loop.
 template <int NP>
 struct PassCfg {
-    static constexpr int WB = (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
+    static constexpr int WB = NP == 0 ? kWavesPerBlock : (NP <= 4) ? 64 : 32;   // walkers per pass (LDS: WB*NP*64 B)
+    static constexpr int NPA = NP > 0 ? NP : RVK_MAX_PLANETS;                   // planet slots per walker
 };
 
 template <int NP, bool MULTI, int SOLVER, bool TP, int SAMPLE, int BLK = kBlock>
@@ -131,7 +134,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                                                          const double *__restrict__ theta, long long n_walkers,
                                                          long long stride, int wb, double *__restrict__ out,
                                                          PostArgs post, SampleArgs sa) {
-    constexpr int WB = PassCfg<NP>::WB;
+    constexpr int WB = PassCfg<NP>::WB, NPA = PassCfg<NP>::NPA;
+    const int np = NP > 0 ? NP : d.np;
     // SAMPLE & 3: 1 accept / reject of propose_kernel's proposals; 2 proposals made in this kernel
     // + accept / reject; 3 proposals made here, log-posterior out (rvk_stretch_propose).
     // SAMPLE & 4 (ALLP): every prior kind in the fused prep (else the basic kinds only);
@@ -143,8 +147,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     constexpr bool CONV = (SAMPLE & 8) != 0;
     constexpr bool EXT = CONV || (SAMPLE & 4) != 0;
     constexpr int WF = FUSE ? BLK / 64 : 1;   // fused: one walker per wave per pass (launch_sample_fused)
-    __shared__ PlanetK pks[WB][NP];
-    __shared__ int okp[WB][NP];
+    __shared__ PlanetK pks[WB][NPA];
+    __shared__ int okp[WB][NPA];
     __shared__ double fq[WF][kFuseMaxD], fx[WF][kFuseMaxD], ff[WF][kFuseMaxPFull];
     constexpr int FP = FUSE ? kFuseMaxPFull : 1, FS = FUSE ? kFuseMaxPrior : 1;
     __shared__ int fcol[FP];
@@ -213,8 +217,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
         // prep (the table fill above lands under the same barrier)
         if constexpr (!FUSE) {
-        for (int k = threadIdx.x; k < nb * NP; k += BLK) {
-            const int j = k / NP, p = k - j * NP;
+        for (int k = threadIdx.x; k < nb * np; k += BLK) {
+            const int j = k / np, p = k - j * np;
             const long long w = base + j;
             const double *p5 = theta + w * stride + 5 * p;
             PlanetK pk;
@@ -315,15 +319,19 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 lau_s = sa.lau[w];
             }
             bool all_ok = true;
+            if constexpr (NP > 0) {
 #pragma unroll
-            for (int p = 0; p < NP; ++p) all_ok &= okp[j][p] != 0;
+                for (int p = 0; p < NP; ++p) all_ok &= okp[j][p] != 0;
+            } else {
+                for (int p = 0; p < np; ++p) all_ok &= okp[j][p] != 0;
+            }
             double res = -INFINITY;
             if (all_ok && lpw != -INFINITY) {
-            const double *g = row + 5 * NP;
+            const double *g = row + 5 * np;
             const double *jit = g + n_inst;
             const double gd = jit[n_inst], gdd = jit[n_inst + 1];
             const double g0 = g[0], j0 = jit[0] * jit[0];
-            PlanetK pk[NP];
+            PlanetK pk[NP > 0 ? NP : 1];
 #pragma unroll
             for (int p = 0; p < NP; ++p) pk[p] = NP >= RVK_PK_SGPR ? uniform_pk(pks[j][p]) : pks[j][p];
             double chi2 = 0.0, prod = 0.5;   // prod * 2^expo = running product of s^2
@@ -341,8 +349,12 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                         }
                     }
                     double rv = gam - vel;   // the residual itself: each planet's K * (...) lands in one FMA
+                    if constexpr (NP > 0) {
 #pragma unroll
-                    for (int p = 0; p < NP; ++p) rv = planet_rv<SOLVER>(pk[p], t, tab, rv);
+                        for (int p = 0; p < NP; ++p) rv = planet_rv<SOLVER>(pk[p], t, tab, rv);
+                    } else {
+                        for (int p = 0; p < np; ++p) rv = planet_rv<SOLVER>(pks[j][p], t, tab, rv);
+                    }
                     if (TREND) {
                         const double dt = t - d.t0;
                         rv += __builtin_fma(gd, dt, gdd * (dt * dt));
@@ -612,28 +624,46 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
     }
 }
 
-// Posterior predictive (fit.py:2690-2939): one wave per sample, lanes over times.
+// Posterior predictive (fit.py:2690-2939): one wave per sample, lanes over times.  `sel`: bit p
+// = planet p included; NP = the selected count (1..8 specialised, 0 = any count, the planet
+// constants in LDS).
 template <int NP, int SOLVER>
 __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restrict__ tq, const int32_t *__restrict__ iq,
                                                          long long n_t, int n_planets_total, int n_inst, int par,
                                                          double t0, const double *__restrict__ theta,
                                                          long long n_samples, long long stride, unsigned what,
-                                                         const SC *__restrict__ gtab, double *__restrict__ out) {
+                                                         unsigned long long sel, const SC *__restrict__ gtab,
+                                                         double *__restrict__ out) {
     __shared__ SC tab[kTabN];
+    __shared__ PlanetK pkl[NP == 0 ? kWavesPerBlock : 1][NP == 0 ? RVK_MAX_PLANETS : 1];
     load_tab(tab, gtab);
     const int lane = threadIdx.x & 63;
-    const long long wave0 = (long long)blockIdx.x * kWavesPerBlock +
-                            __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long wave0 = (long long)blockIdx.x * kWavesPerBlock + wv;
     const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
+    const int nsel = __builtin_popcountll(sel);
     for (long long s = wave0; s < n_samples; s += nwaves) {
         const double *row = theta + s * stride;
         PlanetK pk[NP > 0 ? NP : 1];
         bool ok = true;
+        if constexpr (NP > 0) {
 #pragma unroll
-        for (int q = 0; q < NP; ++q) {   // q-th selected planet = q-th set bit of `what`
-            unsigned m = what & RVK_PRED_PLANETS;
-            for (int k = 0; k < q; ++k) m &= m - 1u;
-            ok &= planet_consts(par, row + 5 * __builtin_ctz(m), pk[q]);
+            for (int q = 0; q < NP; ++q) {   // q-th selected planet = q-th set bit of `sel`
+                unsigned long long m = sel;
+                for (int k = 0; k < q; ++k) m &= m - 1ull;
+                ok &= planet_consts(par, row + 5 * __builtin_ctzll(m), pk[q]);
+            }
+        } else {                             // lane q < nsel: the q-th selected planet, into LDS
+            int okq = 1;
+            if (lane < nsel) {
+                unsigned long long m = sel;
+                for (int k = 0; k < lane; ++k) m &= m - 1ull;
+                PlanetK q;
+                okq = planet_consts(par, row + 5 * __builtin_ctzll(m), q);
+                pkl[wv][lane] = q;
+            }
+            ok = __builtin_amdgcn_ballot_w64(!okq) == 0;
+            wave_lds_sync();
         }
         const double *g = row + 5 * n_planets_total;
         const double *jit = g + n_inst;
@@ -641,8 +671,12 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restric
         for (long long j = lane; j < n_t; j += 64) {
             double v = 0.0;
             const double t = tq[j];
+            if constexpr (NP > 0) {
 #pragma unroll
-            for (int p = 0; p < NP; ++p) v = planet_rv<SOLVER>(pk[p], t, tab, v);
+                for (int p = 0; p < NP; ++p) v = planet_rv<SOLVER>(pk[p], t, tab, v);
+            } else {
+                for (int p = 0; p < nsel; ++p) v = planet_rv<SOLVER>(pkl[wv][p], t, tab, v);
+            }
             if (what & RVK_PRED_TREND) {
                 const double dt = t - t0;
                 v += __builtin_fma(gd, dt, gdd * (dt * dt));
@@ -650,6 +684,7 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restric
             if (what & RVK_PRED_GAMMA) v += g[iq ? iq[j] : 0];
             out[s * n_t + j] = ok ? v : NAN;
         }
+        if constexpr (NP == 0) wave_lds_sync();   // pkl is rewritten for the wave's next sample
     }
 }
 
@@ -720,7 +755,7 @@ inline int choose_lpw(int forced, int np, int n, long long W) {
 template <int NP, bool MULTI, int SOLVER, bool TP>
 void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, long long W, long long stride,
                double *out, PostArgs post) {
-    if (SOLVER == 0) {
+    if constexpr (SOLVER == 0 && NP > 0) {   // (the generic NP = 0 kernel has the one-wave layout only)
         const int lpw = choose_lpw(d.lpw, NP, n, W);
         if (lpw == 32) return launch_seg<NP, MULTI, TP, 32>(st, d, n, ni, th, W, stride, out, post);
         if (lpw == 16) return launch_seg<NP, MULTI, TP, 16>(st, d, n, ni, th, W, stride, out, post);
@@ -773,7 +808,7 @@ loglike_launch_t pick_ll_s(int np) {
         case 6: return launch_ll<6, MULTI, SOLVER, TP>;
         case 7: return launch_ll<7, MULTI, SOLVER, TP>;
         case 8: return launch_ll<8, MULTI, SOLVER, TP>;
-        default: return nullptr;
+        default: return np <= RVK_MAX_PLANETS ? launch_ll<0, MULTI, SOLVER, TP> : nullptr;
     }
 }
 
@@ -802,7 +837,7 @@ sample_launch_t pick_sample_s(int np) {
             case 6: return launch_sample<6, MULTI, TP>;
             case 7: return launch_sample<7, MULTI, TP>;
             case 8: return launch_sample<8, MULTI, TP>;
-            default: return nullptr;
+            default: return np <= RVK_MAX_PLANETS ? launch_sample<0, MULTI, TP> : nullptr;
         }
     } else {
         switch (np) {
@@ -929,8 +964,8 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
                        double t0, int32_t device) {
     if (n < 0 || (n > 0 && (!time || !vel || !velerr)))
         return fail(RVK_E_ARG, "n_epochs must be >= 0 with non-NULL data (0 = model-only handle for rvk_predict)");
-    if (n_planets < 1 || n_planets > RVK_MAX_PLANETS) return fail(RVK_E_ARG, "n_planets must be in [1, 8]");
-    if (n_inst < 1 || n_inst > RVK_MAX_INST) return fail(RVK_E_ARG, "n_inst must be in [1, 16]");
+    if (n_planets < 1 || n_planets > RVK_MAX_PLANETS) return fail(RVK_E_ARG, "n_planets must be in [1, 32]");
+    if (n_inst < 1 || n_inst > RVK_MAX_INST) return fail(RVK_E_ARG, "n_inst must be in [1, 64]");
     if (par < 0 || par > 3) return fail(RVK_E_ARG, "unknown parameterisation code");
     if (n > 0 && n_inst > 1 && !inst_idx) return fail(RVK_E_ARG, "inst_idx is required when n_inst > 1");
     std::vector<int32_t> inst((size_t)n, 0);
@@ -1079,28 +1114,43 @@ int rvk_predict_device(rvk_handle *h, const double *d_theta, int64_t S, int64_t 
     if (S == 0 || n_t == 0) return RVK_OK;
     if (!d_theta || !d_t || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
     if ((what & RVK_PRED_GAMMA) && h->n_inst > 1 && !d_inst) return fail(RVK_E_ARG, "inst required for GAMMA");
-    unsigned planets = what & RVK_PRED_PLANETS & ((1u << h->n_planets) - 1u);
-    const int nsel = __builtin_popcount(planets);
-    what = (what & ~RVK_PRED_PLANETS) | planets;
+    // planet selection: bits 0-7, every planet, or one planet by index (include/rvk.h)
+    const unsigned long long all = (1ull << h->n_planets) - 1ull;
+    unsigned long long sel = (unsigned long long)(what & RVK_PRED_PLANETS);
+    if (what & RVK_PRED_ALL_PLANETS) sel = all;
+    if (what & 0x0800u) {
+        const unsigned p = (what >> 16) & 0xFFu;
+        if ((int)p >= h->n_planets) return fail(RVK_E_ARG, "RVK_PRED_PLANET index out of range");
+        sel |= 1ull << p;
+    }
+    sel &= all;
+    const int nsel = __builtin_popcountll(sel);
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipSetDevice(h->device));
     dim3 grid = wave_grid(S);
-#define PRED_CASE(K)                                                                                           \
-    case K:                                                                                                    \
-        if (h->solver == 1)                                                                                    \
-            hipLaunchKernelGGL((predict_kernel<K, 1>), grid, dim3(kBlock), 0, st, d_t, d_inst, (long long)n_t,  \
-                               h->n_planets, h->n_inst, h->par, h->t0, d_theta, (long long)S, (long long)stride,\
-                               what, h->d_tab, d_out);                                                         \
-        else                                                                                                   \
-            hipLaunchKernelGGL((predict_kernel<K, 0>), grid, dim3(kBlock), 0, st, d_t, d_inst, (long long)n_t,  \
-                               h->n_planets, h->n_inst, h->par, h->t0, d_theta, (long long)S, (long long)stride,\
-                               what, h->d_tab, d_out);                                                         \
-        break;
+#define PRED_LAUNCH(K)                                                                                          \
+    do {                                                                                                        \
+        if (h->solver == 1)                                                                                     \
+            hipLaunchKernelGGL((predict_kernel<K, 1>), grid, dim3(kBlock), 0, st, d_t, d_inst, (long long)n_t,   \
+                               h->n_planets, h->n_inst, h->par, h->t0, d_theta, (long long)S, (long long)stride, \
+                               what, sel, h->d_tab, d_out);                                                     \
+        else                                                                                                    \
+            hipLaunchKernelGGL((predict_kernel<K, 0>), grid, dim3(kBlock), 0, st, d_t, d_inst, (long long)n_t,   \
+                               h->n_planets, h->n_inst, h->par, h->t0, d_theta, (long long)S, (long long)stride, \
+                               what, sel, h->d_tab, d_out);                                                     \
+    } while (0)
     switch (nsel) {
-        PRED_CASE(0) PRED_CASE(1) PRED_CASE(2) PRED_CASE(3) PRED_CASE(4) PRED_CASE(5) PRED_CASE(6)
-        PRED_CASE(7) PRED_CASE(8)
+        case 1: PRED_LAUNCH(1); break;
+        case 2: PRED_LAUNCH(2); break;
+        case 3: PRED_LAUNCH(3); break;
+        case 4: PRED_LAUNCH(4); break;
+        case 5: PRED_LAUNCH(5); break;
+        case 6: PRED_LAUNCH(6); break;
+        case 7: PRED_LAUNCH(7); break;
+        case 8: PRED_LAUNCH(8); break;
+        default: PRED_LAUNCH(0); break;   // none selected (trend / gamma only), or more than 8
     }
-#undef PRED_CASE
+#undef PRED_LAUNCH
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

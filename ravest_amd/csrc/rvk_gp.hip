@@ -129,7 +129,7 @@ struct GpLds {
 };
 
 template <int NW>
-__device__ __forceinline__ GpLds carve(void *smem, int nt) {
+__device__ __forceinline__ GpLds carve(void *smem, int nt, int np) {
     GpLds L;
     float *f = reinterpret_cast<float *>(smem);
     L.uph = f;
@@ -153,8 +153,8 @@ __device__ __forceinline__ GpLds carve(void *smem, int nt) {
     static_assert((3 * NW * sizeof(double)) % 16 == 0, "table alignment");
     L.tab = reinterpret_cast<SC *>(L.red + 3 * NW);
     L.pk = reinterpret_cast<PlanetK *>(L.tab + kTabN);
-    L.ok = reinterpret_cast<int *>(L.pk + RVK_MAX_PLANETS);
-    L.slot = reinterpret_cast<short *>(L.ok + RVK_MAX_PLANETS);
+    L.ok = reinterpret_cast<int *>(L.pk + np);
+    L.slot = reinterpret_cast<short *>(L.ok + ((np + 3) & ~3));
     return L;
 }
 
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
     constexpr int NT = 64 * NW;
     extern __shared__ double smem_d[];
     const int nt = (n + TB - 1) / TB, npad = nt * TB;
-    const GpLds L = carve<NW>(smem_d, nt);
+    const GpLds L = carve<NW>(smem_d, nt, np);
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // Tile rows are owned round-robin by waves, rotated per workgroup: in the last steps only one
@@ -783,9 +783,8 @@ size_t gp_lds_bytes(int n, int np, int nw) {
     size_t b = sizeof(float) * 2 * (size_t)nt * TB;
     b += sizeof(float) * ((size_t)(nt - 1) * TILE + TB * RS + 2 * (size_t)nt * TB + TB) + 16;
     b += sizeof(double) * 3 * nw;
-    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
+    b += sizeof(SC) * kTabN + sizeof(PlanetK) * (size_t)np + sizeof(int) * (size_t)((np + 3) & ~3) + 16;
     b += sizeof(short) * (size_t)nt * nt;
-    (void)np;
     return b;
 }
 
@@ -1002,7 +1001,7 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     const Gp64Shape s64 = gp64_shape(h->n);
     g->launch64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, false, s64);
     g->cond64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, true, s64);
-    g->lds64 = gp64_lds_bytes(h->n, s64.nw);
+    g->lds64 = gp64_lds_bytes(h->n, h->n_planets, s64.nw);
     g->grid64 = (unsigned)prop.multiProcessorCount;
     g->w64stride = gp64_work_doubles(h->n);
     HIPCHK(hipMalloc(&g->d_work64, sizeof(double) * (size_t)g->w64stride * g->grid64));

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     double *red = li + TILE;          // [2 NW]
     SC *tab = reinterpret_cast<SC *>(red + 2 * NW);
     PlanetK *pks = reinterpret_cast<PlanetK *>(tab + kTabN);
-    int *oks = reinterpret_cast<int *>(pks + RVK_MAX_PLANETS);
+    int *oks = reinterpret_cast<int *>(pks + np);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wr = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave owns tile rows wr, wr + NW, ...
     const EpochData &d = a.d;
@@ -600,10 +600,10 @@ Gp64Shape gp64_shape(int n) {
     return nt <= 16 ? Gp64Shape{8, 3} : Gp64Shape{8, 5};   // 7 row-owning waves + the factor wave
 }
 
-size_t gp64_lds_bytes(int n, int nw) {
+size_t gp64_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * (3 * (size_t)nt * TB + TB * FS + TILE + 2 * (size_t)nw);
-    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)RVK_MAX_PLANETS + 16;
+    b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
     return b;
 }
 

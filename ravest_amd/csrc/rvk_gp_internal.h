@@ -41,7 +41,7 @@ struct Gp64Shape {
     int nw, maxr;
 };
 Gp64Shape gp64_shape(int n);
-size_t gp64_lds_bytes(int n, int nw);
+size_t gp64_lds_bytes(int n, int np, int nw);
 long long gp64_work_doubles(int n);        // per workgroup
 // nullptr if unsupported (np outside 1..8)
 gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape sh);

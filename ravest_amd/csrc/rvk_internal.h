@@ -27,6 +27,7 @@ struct EpochData {
     double t0;            // Trend reference time (model.py:486,491)
     int par;              // parameterisation code (RVK_PAR_*)
     int lpw;              // lanes per walker: 0 = chosen per launch, else 64 / 32 / 16 (RVK_OPT_LPW)
+    int np;               // planets (the generic kernels' runtime count; the others are specialised)
 };
 
 // Optional log-posterior epilogue of the log-likelihood kernel (fit.py:3461-3495):
@@ -119,6 +120,6 @@ struct rvk_handle {
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW
 
-    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw}; }
+    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw, n_planets}; }
     int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }
 };

@@ -13,8 +13,8 @@
 
 namespace rvk {
 
-constexpr int kMaxPFull = 5 * RVK_MAX_PLANETS + 2 * RVK_MAX_INST + 2;   // 74
-constexpr int kMaxPFullPad = 80;
+constexpr int kMaxPFull = 5 * RVK_MAX_PLANETS + 2 * RVK_MAX_INST + 2;   // 290
+constexpr int kMaxPFullPad = (kMaxPFull + 7) / 8 * 8;
 
 struct PriorSlot {
     int32_t kind, src;

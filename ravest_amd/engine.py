@@ -69,10 +69,17 @@ class RVEngine:
                                                   out.data_ptr(), stream.cuda_stream))
 
     def _what(self, planets, trend, gamma) -> int:
-        planets = range(self.n_planets) if planets is None else planets
+        """include/rvk.h's component mask: every planet, planets 0-7 by bit, or one planet >= 8 by index."""
+        planets = list(range(self.n_planets)) if planets is None else sorted({int(p) for p in planets})
         what = 0
-        for p in planets:
-            what |= 1 << int(p)
+        if planets and planets == list(range(self.n_planets)):
+            what |= _lib.PRED_ALL_PLANETS
+        else:
+            high = [p for p in planets if p >= 8]
+            if len(high) > 1:
+                raise ValueError("rvk_predict selects planets >= 8 one at a time (or all planets)")
+            for p in planets:
+                what |= (1 << p) if p < 8 else _lib.pred_planet(p)
         if trend:
             what |= _lib.PRED_TREND
         if gamma:
@@ -110,6 +117,10 @@ class RVEngine:
     def set_lanes_per_walker(self, lpw: int) -> None:
         """0 = chosen per launch (default); 64, 32 or 16 lanes of a wave per walker (RVK_OPT_LPW)."""
         _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_LPW, int(lpw)))
+
+    def set_graph(self, on: bool) -> None:
+        """RVK_OPT_GRAPH: the device stretch move replays a cached HIP graph per block of steps."""
+        _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_GRAPH, int(bool(on))))
 
     def reserve(self, max_walkers: int) -> None:
         _lib.check(_lib.load().rvk_reserve(self._h, int(max_walkers)))

@@ -208,6 +208,9 @@ def _host_array(shape) -> np.ndarray:
 def _copy(dst: np.ndarray, src) -> None:
     """dst[...] = src with torch's multi-threaded copy (src: a host tensor or array)."""
     import torch
+    if os.environ.get("RVK_HOST_COPY") == "numpy":          # experiment hook: one thread
+        np.copyto(dst, src.numpy() if isinstance(src, torch.Tensor) else src)
+        return
     torch.from_numpy(dst).copy_(src if isinstance(src, torch.Tensor) else torch.from_numpy(np.asarray(src)))
 
 
@@ -506,11 +509,19 @@ class _DevicePipeline(_SamplerBase):
         ch.start, ch.n, ch.slot, ch.copied = self._dev_iter, n, slot, None
         if self._trace is not None:
             self._trace.append(("enqueue", time.perf_counter()))
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
         self._begin_chunk(ch)
         chain_d, lnp_d = self._dbuf[slot]
+        if self._trace is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(stream)
         self._run_chunk(ch, chain_d, lnp_d, stream)
         if self._trace is not None:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record(stream)
             self._trace.append(("launched", time.perf_counter()))
+            self._gpu_trace = getattr(self, "_gpu_trace", []) + [(e0, e1, e2)]
         self._dev_iter += n
         if self._cuda:
             computed = torch.cuda.Event()
@@ -526,8 +537,10 @@ class _DevicePipeline(_SamplerBase):
                                               cs.cuda_stream))
                 _lib.check(L.rvk_copy_to_host(lnp_d.data_ptr(), sl.data_ptr(), n * lnp_d[0].numel() * 8, wg,
                                               cs.cuda_stream))
+            if os.environ.get("RVK_NO_EGRESS"):   # experiment hook: no chain copy-out (timing only)
+                sc = None
             with torch.cuda.stream(cs):
-                if self._keep_host and not wg:
+                if self._keep_host and not wg and sc is not None:
                     sc[:n].copy_(chain_d[:n], non_blocking=True)
                     sl[:n].copy_(lnp_d[:n], non_blocking=True)
                 ss.copy_(self._status, non_blocking=True)

@@ -27,8 +27,8 @@ CONFIGS = {
     5: dict(seed=5, n_planets=1, n_epochs=512, n_walkers=4096, n_inst=1),   # + quasi-periodic GP
 }
 
-LETTERS = "bcdefghi"
-INSTRUMENTS = ["HARPS", "HIRES", "ESPRESSO", "CORALIE"]
+LETTERS = [c for c in "bcdefghijklmnopqrstuvwxyz"] + [f"z{k}" for k in range(8)]   # 33 planet names
+INSTRUMENTS = ["HARPS", "HIRES", "ESPRESSO", "CORALIE"] + [f"INST{k:02d}" for k in range(60)]
 
 
 @dataclass

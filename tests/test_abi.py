@@ -49,7 +49,7 @@ def test_bad_arguments_fail_loudly():
     dp = C.POINTER(C.c_double)
     t = np.linspace(0, 10, 8)
     # n_planets out of range is rejected before any device work
-    h = L.rvk_create(t.ctypes.data_as(dp), t.ctypes.data_as(dp), t.ctypes.data_as(dp), None, 8, 1, 9, 0, 0.0, -1)
+    h = L.rvk_create(t.ctypes.data_as(dp), t.ctypes.data_as(dp), t.ctypes.data_as(dp), None, 8, 1, 33, 0, 0.0, -1)
     assert not h and "n_planets" in _lib.last_error()
     h = L.rvk_create(t.ctypes.data_as(dp), t.ctypes.data_as(dp), t.ctypes.data_as(dp), None, 8, 2, 1, 0, 0.0, -1)
     assert not h and "inst_idx" in _lib.last_error()

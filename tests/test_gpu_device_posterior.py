@@ -159,3 +159,31 @@ def test_fused_sampler_equals_two_kernel_path(monkeypatch, what, rng):
     assert a1.sum() > 0
     lpost, _ = _fused_case(what, W)
     assert_ll_close(l1[-1], lpost.log_probability_batch(c1[-1]), what=f"fused-{what}-last-step")
+
+
+def test_many_planets_instruments_posterior_and_sampler():
+    """10 planets and 20 instruments (the generic > 8-planet kernel; P_full = 92, so the
+    two-kernel half-step): the device log-posterior equals the host path, and the device
+    sampler reproduces the host stretch move draw for draw (emcee's RandomState stream)."""
+    from ravest_amd.synth import make_dataset
+    ds = make_dataset(10, 120, 20, seed=31, trend=False)
+    free = [n for n in ds.names if n not in ("gd", "gdd")]
+    priors = {}
+    for n in free:
+        v, base = ds.truth[n], n.split("_")[0]
+        priors[n] = (P.EccentricityUniform(0.99) if base == "e" else P.Uniform(-np.pi, np.pi) if base == "w"
+                     else P.HalfNormal(5.0) if base == "jit" else P.Uniform(v - 0.5 * abs(v) - 1.0, v + 0.5 * abs(v) + 1.0))
+    lpost = LogPosterior(ds.planet_letters, ds.parameterisation, priors, {"gd": 0.0, "gdd": 0.0}, free, ds.time,
+                         ds.vel, ds.velerr, ds.instrument, ds.unique_instruments, ds.t0)
+    rng = np.random.default_rng(3)
+    x0 = np.array([ds.truth[n] for n in free])[None, :] * (1 + 1e-4 * rng.standard_normal((256, len(free))))
+    dev = lpost.device_posterior()(x0)
+    assert_ll_close(dev, lpost.log_probability_batch(x0), what="np10-ni20-device-vs-host")
+    assert np.all(np.isfinite(dev))
+    W = 256
+    host = EnsembleSampler(W, len(free), lpost.log_probability_batch, seed=np.random.RandomState(5))
+    host.run_mcmc(x0, 10)
+    ds_ = DeviceEnsembleSampler(lpost, W, seed=np.random.RandomState(5), rng="emcee", steps_per_call=4)
+    ds_.run_mcmc(x0, 10)
+    assert np.array_equal(host.naccepted, ds_.naccepted)
+    np.testing.assert_allclose(ds_.get_chain(), host.get_chain(), rtol=1e-12, atol=0)

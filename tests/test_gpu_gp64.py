@@ -64,7 +64,8 @@ def _walkers(ds, W, seed, **kw):
                                                 (32, 1, 1, "P K e w Tp", False), (33, 1, 1, "P K e w Tp", False),
                                                 (1, 1, 1, "P K e w Tp", False),
                                                 (700, 1, 1, "P K e w Tp", False),
-                                                (1024, 2, 2, "P K secosw sesinw Tc", True)])
+                                                (1024, 2, 2, "P K secosw sesinw Tc", True),
+                                                (150, 10, 12, "P K e w Tc", True)])   # > 8 planets
 def test_fp64_loglike_vs_oracle(n, np_, ni, par, trend):
     from ravest_amd.synth import make_dataset
     ds = make_dataset(np_, n, ni, seed=150 + n, parameterisation=par, trend=trend)

@@ -210,7 +210,9 @@ def test_large_batch_mask_and_determinism():
     assert (~np.isfinite(a)).sum() >= int(0.02 * len(a) * 2 / 3) - 2
 
 
-@pytest.mark.parametrize("np_,ni,par", [(5, 4, "P K e w Tc"), (8, 3, "P K secosw sesinw Tp"), (4, 1, "P K e w Tp")])
+@pytest.mark.parametrize("np_,ni,par", [(5, 4, "P K e w Tc"), (8, 3, "P K secosw sesinw Tp"), (4, 1, "P K e w Tp"),
+                                        (10, 20, "P K e w Tp"), (9, 17, "P K secosw sesinw Tc"),
+                                        (32, 64, "P K e w Tc")])      # generic kernel (> 8 planets), caps
 def test_many_planets_and_instruments_vs_oracle(np_, ni, par):
     from oracle import oracle
     from ravest_amd.engine import RVEngine
