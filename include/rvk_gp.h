@@ -25,7 +25,7 @@
  *                              tinygp with jax_enable_x64, fit.py:39); NaN only where
  *                              the covariance is not positive definite in fp64.
  * An invalid planet gives -inf (the reference's mean-model fail-fast).
- * Epochs: 1 <= n_epochs <= 1024.  Calls on one rvk_gp share its workspaces: keep
+ * Epochs: 1 <= n_epochs <= RVK_GP_MAX_EPOCHS (4096; the fp32 modes run the fp64 factorisation above 1024).  Calls on one rvk_gp share its workspaces: keep
  * them on one stream (or serialise them).
  *
  * hyper row layout [W][hyper_stride] fp64: gp_amp, gp_lambda_e, gp_lambda_p,
@@ -45,7 +45,7 @@ extern "C" {
 
 #define RVK_GP_QUASIPERIODIC 0
 #define RVK_GP_NHYPER        4
-#define RVK_GP_MAX_EPOCHS    1024
+#define RVK_GP_MAX_EPOCHS    4096   /* fp32 factorisation up to 1024 epochs; above, the fp64 one in every mode */
 
 #define RVK_GP_FP32                 0
 #define RVK_GP_FP32_FP64_FALLBACK   1

@@ -971,22 +971,17 @@ static void free_gp(rvk_gp *g) {
     delete g;
 }
 
-static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
-    if (!h) return fail(RVK_E_ARG, "NULL handle");
-    if (kernel != RVK_GP_QUASIPERIODIC) return fail(RVK_E_ARG, "unknown GP kernel type");
-    if (h->n < 1 || h->n > RVK_GP_MAX_EPOCHS) return fail(RVK_E_ARG, "GP needs 1 <= n_epochs <= 1024");
-    g->h = h;
+// The fp32 factorisation's launch shape and workspace (n <= kGpF32MaxEpochs: its column panel
+// lives in LDS).
+static int create_gp32(rvk_gp *g, rvk_handle *h, const hipDeviceProp_t &prop) {
     // experiment hooks (tools/gp_ab.sh), never set in production: waves per walker, workgroups per CU
     int wgpcu = RVK_GP_WGPCU, prefer_nw = 4;
     if (const char *e = getenv("RVK_GP_NW")) prefer_nw = atoi(e);
     if (const char *e = getenv("RVK_GP_WGPCU")) wgpcu = atoi(e) > 1 ? atoi(e) : 1;
     const GpShape sh = gp_shape(h->n, prefer_nw);
     g->launch = pick_gp(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, sh);
-    if (!g->launch) return fail(RVK_E_ARG, "GP supports 1..8 planets");
+    if (!g->launch) return fail(RVK_E_ARG, "GP supports 1..32 planets");
     g->lds = gp_lds_bytes(h->n, h->n_planets, sh.nw);
-    HIPCHK(hipSetDevice(h->device));
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, h->device));
     // workgroups that fit at once (LDS-limited), each with its own workspace
     const size_t per_cu = (size_t)160 * 1024 / g->lds;
     g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > (size_t)wgpcu ? (size_t)wgpcu : per_cu)));
@@ -997,10 +992,24 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     HIPCHK(hipMalloc(&g->d_work, sizeof(float) * (size_t)g->wstride * g->grid));
     HIPCHK(hipMalloc(&g->d_slots, sizeof(short) * slots.size()));
     HIPCHK(hipMemcpy(g->d_slots, slots.data(), sizeof(short) * slots.size(), hipMemcpyHostToDevice));
+    return RVK_OK;
+}
+
+static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
+    if (!h) return fail(RVK_E_ARG, "NULL handle");
+    if (kernel != RVK_GP_QUASIPERIODIC) return fail(RVK_E_ARG, "unknown GP kernel type");
+    if (h->n < 1 || h->n > RVK_GP_MAX_EPOCHS) return fail(RVK_E_ARG, "GP needs 1 <= n_epochs <= 4096");
+    g->h = h;
+    HIPCHK(hipSetDevice(h->device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, h->device));
+    int rc;
+    if (h->n <= kGpF32MaxEpochs && (rc = create_gp32(g, h, prop))) return rc;
     // fp64 path: one 4-wave-per-SIMD workgroup per CU, the whole lower triangle of L per workgroup
     const Gp64Shape s64 = gp64_shape(h->n);
     g->launch64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, false, s64);
     g->cond64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, true, s64);
+    if (!g->launch64 || !g->cond64) return fail(RVK_E_ARG, "GP supports 1..32 planets");
     g->lds64 = gp64_lds_bytes(h->n, h->n_planets, s64.nw);
     g->grid64 = (unsigned)prop.multiProcessorCount;
     g->w64stride = gp64_work_doubles(h->n);
@@ -1030,17 +1039,18 @@ static Gp64Args args64(rvk_gp *g, const double *th, const double *hy, long long 
 static int gp_run(rvk_gp *g, const double *th, const double *hy, long long W, long long stride, long long hs,
                   double *out, GpPost post, hipStream_t st) {
     rvk_handle *h = g->h;
-    if (g->mode != RVK_GP_FP64) {
+    const bool f32 = g->mode != RVK_GP_FP64 && g->launch;   // (n > kGpF32MaxEpochs: fp64 in every mode)
+    if (f32) {
         const unsigned grid = (unsigned)((long long)g->grid < W ? g->grid : W);
         g->launch(st, grid, g->lds, h->epochs(), h->n, h->n_inst, h->n_planets, th, hy, W, stride, hs, g->d_slots,
                   g->d_work, g->wstride, out, post);
         HIPCHK(hipGetLastError());
     }
-    if (g->mode != RVK_GP_FP32) {
+    if (g->mode != RVK_GP_FP32 || !f32) {
         Gp64Args a = args64(g, th, hy, W, stride, hs);
         a.out = out;
         a.post = post;
-        a.gate = g->mode == RVK_GP_FP64 ? nullptr : out;   // fallback: the fp32 NaN walkers only
+        a.gate = f32 ? out : nullptr;                      // fallback: the fp32 NaN walkers only
         const unsigned grid = (unsigned)((long long)g->grid64 < W ? g->grid64 : W);
         g->launch64(st, grid, g->lds64, a);
         HIPCHK(hipGetLastError());

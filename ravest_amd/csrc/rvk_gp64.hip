@@ -20,6 +20,10 @@
 //        S1(k) L(bi, k) = acc(bi, k) X^T (MFMA), stored; r_bi -= L(bi, k) y_k;
 //        S2(k) acc(bi, k+1) -= L(bi, k) L(k+1, k)^T, parked in the workspace slot of
 //              tile (bi, k+1) (the diagonal one stays in its owner's registers).
+//      A wave holds MAXR accumulator rows in registers; when it owns more rows (large n) it
+//      accumulates them MAXR at a time and parks each group in the rows' workspace tiles
+//      (bi, k+1) at once, and S2 reads them back: n is bounded by the LDS vectors, not by
+//      registers (RVK_GP_MAX_EPOCHS).
 //      Accumulators hold the NEGATED transposed tiles in MFMA C/D layout (every MFMA
 //      adds; the C/D layout of a transposed tile is the operand layout of the next
 //      product, so tiles are never reshuffled).  Finished tiles are kept in the
@@ -311,15 +315,11 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         fb[(16 * q + (lane & 15)) * FS + 16 * p + (lane >> 4) + 4 * i] = -A.c[p][q][i];
         };
         if (wr < NA) {
-#pragma unroll
-            for (int q = 0; q < MAXR; ++q) {
-                const int bi = wr + NA * q;
-                if (bi < nt) {
-                    Acc t;
-                    cov_tile(bi, 0, t);
-                    if (bi == 0) put_diag(t);
-                    else park(wk + tix(bi, 0) * TILE, t, lane);
-                }
+            for (int bi = wr; bi < nt; bi += NA) {          // every owned row (also past MAXR: grouped)
+                Acc t;
+                cov_tile(bi, 0, t);
+                if (bi == 0) put_diag(t);
+                else park(wk + tix(bi, 0) * TILE, t, lane);
             }
         }
         __syncthreads();
@@ -350,13 +350,16 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
         } else {
             // ---- the row owners: the next column's accumulation, S1, S2 --------------------------
             Acc nacc[MAXR];
+            const int nown = (nt - wr + NA - 1) / NA;       // rows bi = wr + NA q < nt this wave owns
+            const bool grouped = nown > MAXR;               // more rows than accumulator registers
             for (int k = 0; k < nt; ++k) {
                 G64_MARK(k, 0);
                 G64_MARK(k, 1);
-                if (k + 1 < nt) {
+                for (int qo = 0; qo < nown && k + 1 < nt; qo += MAXR) {   // one trip unless grouped
+                    if (wr + NA * (qo + MAXR - 1) < k + 1) continue;    // the group's rows are finished
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
-                        const int bi = wr + NA * q;
+                        const int bi = wr + NA * (qo + q);
                         if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
                     }
                     // operands: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows at a time,
@@ -368,7 +371,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         constexpr int R = (MAXR - Q0) < 2 ? (MAXR - Q0) : 2;
                         bool any = false;
 #pragma unroll
-                        for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NA * q >= k + 1) && (wr + NA * q < nt);
+                        for (int q = Q0; q < Q0 + R; ++q) any |= (wr + NA * (qo + q) >= k + 1) && (wr + NA * (qo + q) < nt);
                         if (!any || k == 0) return;
                         constexpr int KP = 1, NSET = 4 / KP;   // fragment pairs per register set, sets per tile
                         struct Ops {
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                                 for (int u = 0; u < KP; ++u) o.a[s][u] = ta[(s * 4 + KP * part + u) * 64 + lane];
 #pragma unroll
                             for (int r = 0; r < R; ++r) {
-                                const int bi = wr + NA * (Q0 + r);
+                                const int bi = wr + NA * (qo + Q0 + r);
                                 const bool live = bi >= k + 1 && bi < nt;
                                 const double2 *tb = reinterpret_cast<const double2 *>(wk + tix(live ? bi : k + 1, j) * TILE);
 #pragma unroll
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         auto consume = [&](const Ops &o) {
 #pragma unroll
                             for (int r = 0; r < R; ++r) {
-                                const int bi = wr + NA * (Q0 + r);
+                                const int bi = wr + NA * (qo + Q0 + r);
                                 if (bi >= k + 1 && bi < nt) {
                                     Acc &acc = nacc[Q0 + r];
 #pragma unroll
@@ -425,6 +428,13 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
                     if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
                     if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
+                    if (grouped) {                          // park the group: S2 reads it back
+#pragma unroll
+                        for (int q = 0; q < MAXR; ++q) {
+                            const int bi = wr + NA * (qo + q);
+                            if (bi >= k + 1 && bi < nt) park(wk + tix(bi, k + 1) * TILE, nacc[q], lane);
+                        }
+                    }
                 }
                 G64_MARK(k, 2);
                 __syncthreads();                            // B1: -X and y_k published
@@ -449,8 +459,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) yv[p][i] = Lr[k * TB + 16 * p + (lane >> 4) + 4 * i];
-#pragma unroll
-                for (int q = 0; q < MAXR; ++q) {
+                for (int q = 0; q < nown; ++q) {
                     const int bi = wr + NA * q;
                     if (bi > k && bi < nt) {
                         double *T = wk + tix(bi, k) * TILE;
@@ -497,21 +506,33 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
             {
                 double af[2][8];
                 load_frags(wk + tix(k + 1, k) * TILE, af, lane);
+                auto s2 = [&](Acc &acc, int bi) {
+                    double bf[2][8];
+                    load_frags(wk + tix(bi, k) * TILE, bf, lane);
 #pragma unroll
-                for (int q = 0; q < MAXR; ++q) {
-                    const int bi = wr + NA * q;
-                    if (bi > k && bi < nt) {
-                        double bf[2][8];
-                        load_frags(wk + tix(bi, k) * TILE, bf, lane);
+                    for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-                        for (int kk = 0; kk < 8; ++kk)
+                        for (int p = 0; p < 2; ++p)
 #pragma unroll
-                            for (int p = 0; p < 2; ++p)
+                            for (int qq = 0; qq < 2; ++qq)
+                                acc.c[p][qq] = mfma64(af[p][kk], bf[qq][kk], acc.c[p][qq]);
+                    if (bi == k + 1) put_diag(acc);
+                    else park(wk + tix(bi, k + 1) * TILE, acc, lane);
+                };
+                if (!grouped) {
 #pragma unroll
-                                for (int qq = 0; qq < 2; ++qq)
-                                    nacc[q].c[p][qq] = mfma64(af[p][kk], bf[qq][kk], nacc[q].c[p][qq]);
-                        if (bi == k + 1) put_diag(nacc[q]);
-                        else park(wk + tix(bi, k + 1) * TILE, nacc[q], lane);
+                    for (int q = 0; q < MAXR; ++q) {
+                        const int bi = wr + NA * q;
+                        if (bi > k && bi < nt) s2(nacc[q], bi);
+                    }
+                } else {
+                    for (int q = 0; q < nown; ++q) {
+                        const int bi = wr + NA * q;
+                        if (bi > k && bi < nt) {
+                            Acc acc;
+                            unpark(wk + tix(bi, k + 1) * TILE, acc, lane);
+                            s2(acc, bi);
+                        }
                     }
                 }
             }

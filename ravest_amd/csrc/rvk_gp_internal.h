@@ -7,6 +7,10 @@
 
 namespace rvk {
 
+// The fp32 factorisation keeps a column panel of the walker's factor in LDS: up to this many
+// epochs (the fp64 factorisation, its panels in the workspace, goes to RVK_GP_MAX_EPOCHS).
+constexpr int kGpF32MaxEpochs = 1024;
+
 // Optional GP log-posterior epilogue (GPLogPosterior.log_probability, fit.py:7836-7901):
 // lp == nullptr: out = GP log-likelihood.  Otherwise lp[w] / lhp[w] are the walker's
 // log-prior and log-hyperprior (lp[w] = -inf: rejected before the likelihood -- negative

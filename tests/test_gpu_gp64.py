@@ -307,3 +307,33 @@ def test_gp_device_sampler_matches_host_sampler():
     ph = DeviceEnsembleSampler(gp, W, seed=7)           # device Philox draws
     ph.run_mcmc(x0, 6)
     assert np.all(np.isfinite(ph.get_log_prob()))
+
+
+@pytest.mark.parametrize("n,np_,ni", [(1500, 1, 1), (2048, 2, 2), (4096, 1, 1)])
+def test_fp64_above_the_fp32_limit(n, np_, ni):
+    """n > 1024 (the fp32 kernel's LDS panel limit): the fp64 factorisation with its accumulator
+    rows grouped through the workspace, fp64 1e-9 against the oracle; the fp32 modes run the
+    same fp64 kernel there (identical values)."""
+    from ravest_amd.synth import make_dataset
+    ds = make_dataset(np_, n, ni, seed=500 + n, trend=True)
+    th, hy = _walkers(ds, 6 if n > 2048 else 12, n)
+    ll = _gp(ds, "fp64").batch(th, hy)
+    ref = _oracle(ds, th, hy)
+    _check(ll, ref, RTOL64, f"n{n}")
+    assert np.isfinite(ref).sum() >= len(ref) - 2
+    assert np.array_equal(_gp(ds, "fp32+fp64").batch(th, hy), ll, equal_nan=True)
+    assert np.array_equal(_gp(ds, "fp32").batch(th, hy), ll, equal_nan=True)
+
+
+def test_gp_condition_above_the_fp32_limit():
+    from oracle import gp_oracle
+    from ravest_amd.synth import make_dataset
+    ds = make_dataset(1, 1500, 1, seed=1501, trend=True)
+    th, hy = _walkers(ds, 6, 1501)
+    tq = np.linspace(ds.time.min() - 5, ds.time.max() + 5, 120)
+    got = _gp(ds, "fp64").condition(th, hy, tq)
+    ref = gp_oracle.gp_condition(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th, hy, tq)
+    ok = ~np.isnan(ref).all(axis=1)
+    assert np.array_equal(np.isnan(got).all(axis=1), ~ok)
+    scale = np.max(np.abs(ref[ok]), axis=1, keepdims=True)
+    assert np.all(np.abs(got[ok] - ref[ok]) <= 1e-8 * scale)
