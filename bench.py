@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sampler", action="store_true", help="skip the device stretch-move measurement")
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
-    ap.add_argument("--streams", type=int, default=1, help="independent streams per graph")
+    ap.add_argument("--streams", type=int, default=1, help="independent streams per graph (--launch graph)")
+    ap.add_argument("--launch", choices=["eager", "graph"], default="graph",
+                    help="timed loop: G-step HIP graph replays (default) or back-to-back stream launches")
     ap.add_argument("--no-gp", action="store_true", help="skip the config-5 GP likelihood measurement")
     ap.add_argument("--no-predictive", action="store_true", help="skip the posterior-predictive measurement")
     ap.add_argument("--no-configs", action="store_true", help="skip the config-3 / config-4 sub-measurements")
@@ -612,32 +614,55 @@ def main():
         eng.loglike(theta)
     host_ms = (time.perf_counter() - th0) / 10 * 1e3
 
-    # ---- the timed steps: G-step HIP graphs, S independent streams per graph ------------
+    # ---- the timed steps -------------------------------------------------------------------
+    # graph (default): G-step HIP graphs replayed (S independent streams per graph); eager: K
+    # stream-ordered launches issued back to back through the C-ABI entry point (ctypes call
+    # pre-bound).  Measured on MI355X, config 2: at K = 20 (one replay) graph 8.6-8.7 us vs
+    # eager 8.9 us wall per step (eager's kernels run 0.25 us shorter, its host issue costs
+    # more); at K = 200 both 7.6 us.  N > 1: one all-gather of the G steps' log-probs every G steps.
     G = max(1, min(args.graph_steps, args.steps))
     while args.steps % G:                            # time exactly K steps
         G -= 1
     S = max(1, args.streams)
-    nset = 2                                         # two output sets: replay r+1 overlaps gather r
+    nset = 2                                         # two output sets: group r+1 overlaps gather r
     outs = [torch.empty(G, W, dtype=torch.float64, device=dev) for _ in range(nset)]
     gath = [torch.empty(world * G * W, dtype=torch.float64, device=dev) for _ in range(nset)] if world > 1 else None
+    from ravest_amd import _lib
+    ll_fn = _lib.load().rvk_loglike_device
+    call_args = [[(eng._h, th_d.data_ptr(), W, th_d.stride(0), outs[k][j].data_ptr(), stream.cuda_stream)
+                  for j in range(G)] for k in range(nset)]
+
+    def run_group(k):
+        for a in call_args[k]:
+            if ll_fn(*a):
+                _lib.check(-1)
+
     graphs = []
-    cap = torch.cuda.Stream(dev)
-    side = [torch.cuda.Stream(dev) for _ in range(S)]
+    if args.launch == "graph":
+        cap = torch.cuda.Stream(dev)
+        side = [torch.cuda.Stream(dev) for _ in range(S)]
+        for k in range(nset):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                for st in side:
+                    st.wait_stream(cap)
+                for j in range(G):
+                    eng.loglike_device(th_d, outs[k][j], side[j % S])
+                for st in side:
+                    cap.wait_stream(st)
+            graphs.append(g)
+        for g in graphs:                             # warm replays
+            g.replay()
+        launch_group = lambda k: graphs[k].replay()   # noqa: E731  (replayed on `stream`)
+    else:
+        launch_group = run_group
     for k in range(nset):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=cap):
-            for st in side:
-                st.wait_stream(cap)
-            for j in range(G):
-                eng.loglike_device(th_d, outs[k][j], side[j % S])
-            for st in side:
-                cap.wait_stream(st)
-        graphs.append(g)
-    for g in graphs:                                 # warm replays
-        g.replay()
+        launch_group(k)
     torch.cuda.synchronize(dev)
     if not np.array_equal(outs[0][G - 1].cpu().numpy(), ll):
-        raise RuntimeError("graph replay result differs from the eager launch")
+        raise RuntimeError("timed-loop launch result differs from the first eager launch")
+    for _ in range(max(1, args.warmup)):             # the W untimed warmup steps, right before the region
+        eng.loglike_device(th_d, out1, stream)
 
     works = [None] * nset
     rep_ev = []
@@ -652,8 +677,8 @@ def main():
         if works[k] is not None:                     # set k's previous gather must have read it
             works[k].wait()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)                             # the graph is replayed on `stream`
-        graphs[k].replay()
+        a.record(stream)
+        launch_group(k)
         b.record(stream)
         rep_ev.append((a, b))
         if world > 1 and backend == "nccl":
@@ -672,7 +697,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     steps_run = done
-    # average kernel duration inside the timed region: G back-to-back launches per replay
+    # average kernel duration inside the timed region: G back-to-back launches per event pair
     kern_ms = float(sum(a.elapsed_time(b) for a, b in rep_ev)) / steps_run
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -720,14 +745,15 @@ def main():
             "kernel_ms": kern_ms,
             "eager_event_ms": eager_ms,
             "host_path_ms_per_call": host_ms,
-            "launch": f"{G}-step HIP graphs, {S} streams" + (", 1 all-gather per graph (G steps)" if world > 1 else ""),
+            "launch": (f"{G}-step HIP graphs, {S} streams" if args.launch == "graph" else
+                       "back-to-back stream launches") + (f", 1 all-gather per {G} steps" if world > 1 else ""),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "achieved_per_step": alg_bytes / (el / args.steps) / 1e9,
                          "valu": valu, "pmc": pmc_provenance(f"pmc_config{args.config}.json"),
                          "note": "achieved = algorithmic bytes W*(28*N_epochs + 8*P_full + 8) per launch (SURVEY "
-                                 "§8(d)) / average kernel duration (HIP events around each G-launch graph replay "
-                                 "in the timed region / G); traffic = L2 memory-side (fabric) bytes per launch, "
+                                 "§8(d)) / average kernel duration (HIP events around each group of G "
+                                 "launches in the timed region / G); traffic = L2 memory-side (fabric) bytes per launch, "
                                  "FETCH_SIZE x 2 + WRITE_SIZE (PMC; counts Infinity-Cache hits, so an upper bound "
                                  "on HBM bytes: the epoch arrays are re-read from L2/MALL). The binding resource "
                                  "is fp64 VALU issue: 'valu' (PMC counters of the same kernel, null unless "
