@@ -208,7 +208,9 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
     return FactorAcc{quad, dpr, pexp};
 }
 
-template <int NW, int MAXR, bool COND>   // MAXR tile rows per row-owning wave: nt <= MAXR * (NW - 1)
+// MAXR tile rows per row-owning wave; GROUPED: nt > MAXR * (NW - 1), the rows go through the workspace in
+// groups of MAXR (a separate instantiation: the common shape keeps its register allocation)
+template <int NW, int MAXR, bool COND, bool GROUPED>
 __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     constexpr int NT = 64 * NW;
     extern __shared__ double smem64[];
@@ -351,12 +353,12 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
             // ---- the row owners: the next column's accumulation, S1, S2 --------------------------
             Acc nacc[MAXR];
             const int nown = (nt - wr + NA - 1) / NA;       // rows bi = wr + NA q < nt this wave owns
-            const bool grouped = nown > MAXR;               // more rows than accumulator registers
+            constexpr bool grouped = GROUPED;               // more rows than accumulator registers
             for (int k = 0; k < nt; ++k) {
                 G64_MARK(k, 0);
                 G64_MARK(k, 1);
-                for (int qo = 0; qo < nown && k + 1 < nt; qo += MAXR) {   // one trip unless grouped
-                    if (wr + NA * (qo + MAXR - 1) < k + 1) continue;    // the group's rows are finished
+                for (int qo = 0; qo < (grouped ? nown : 1) && k + 1 < nt; qo += MAXR) {   // one trip unless grouped
+                    if (grouped && wr + NA * (qo + MAXR - 1) < k + 1) continue;    // the group's rows are finished
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
                         const int bi = wr + NA * (qo + q);
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
                     if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
                     if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
-                    if (grouped) {                          // park the group: S2 reads it back
+                    if constexpr (grouped) {                // park the group: S2 reads it back
 #pragma unroll
                         for (int q = 0; q < MAXR; ++q) {
                             const int bi = wr + NA * (qo + q);
@@ -459,7 +461,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) yv[p][i] = Lr[k * TB + 16 * p + (lane >> 4) + 4 * i];
-                for (int q = 0; q < nown; ++q) {
+#pragma unroll
+                for (int q = 0; q < (grouped ? nown : MAXR); ++q) {
                     const int bi = wr + NA * q;
                     if (bi > k && bi < nt) {
                         double *T = wk + tix(bi, k) * TILE;
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     if (bi == k + 1) put_diag(acc);
                     else park(wk + tix(bi, k + 1) * TILE, acc, lane);
                 };
-                if (!grouped) {
+                if constexpr (!grouped) {
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
                         const int bi = wr + NA * q;
@@ -601,15 +604,15 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     }
 }
 
-template <int NW, int MAXR, bool COND>
+template <int NW, int MAXR, bool COND, bool GROUPED>
 void launch_gp64(hipStream_t st, unsigned grid, size_t lds, const Gp64Args &a) {
     static size_t allowed = 0;   // dynamic LDS beyond the default needs the attribute
     if (lds > allowed) {
-        (void)hipFuncSetAttribute((const void *)gp64_kernel<NW, MAXR, COND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void *)gp64_kernel<NW, MAXR, COND, GROUPED>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         allowed = lds;
     }
-    hipLaunchKernelGGL((gp64_kernel<NW, MAXR, COND>), dim3(grid), dim3(64 * NW), lds, st, a);
+    hipLaunchKernelGGL((gp64_kernel<NW, MAXR, COND, GROUPED>), dim3(grid), dim3(64 * NW), lds, st, a);
 }
 
 }  // namespace
@@ -618,7 +621,8 @@ namespace rvk {
 
 Gp64Shape gp64_shape(int n) {
     const int nt = (n + TB - 1) / TB;
-    return nt <= 16 ? Gp64Shape{8, 3} : Gp64Shape{8, 5};   // 7 row-owning waves + the factor wave
+    // 7 row-owning waves + the factor wave; beyond 7 x 5 tile rows the rows are grouped
+    return nt <= 16 ? Gp64Shape{8, 3, false} : nt <= 35 ? Gp64Shape{8, 5, false} : Gp64Shape{8, 5, true};
 }
 
 size_t gp64_lds_bytes(int n, int np, int nw) {
@@ -637,8 +641,9 @@ gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape s
     (void)multi;
     (void)tp;
     if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
-    if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true> : launch_gp64<8, 3, false>;
-    return condition ? launch_gp64<8, 5, true> : launch_gp64<8, 5, false>;
+    if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true, false> : launch_gp64<8, 3, false, false>;
+    if (!sh.grouped) return condition ? launch_gp64<8, 5, true, false> : launch_gp64<8, 5, false, false>;
+    return condition ? launch_gp64<8, 5, true, true> : launch_gp64<8, 5, false, true>;
 }
 
 }  // namespace rvk

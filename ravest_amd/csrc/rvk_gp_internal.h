@@ -43,6 +43,7 @@ typedef void (*gp64_launch_t)(hipStream_t, unsigned grid, size_t lds, const Gp64
 
 struct Gp64Shape {
     int nw, maxr;
+    bool grouped;   // more tile rows per wave than maxr (rows accumulated in groups)
 };
 Gp64Shape gp64_shape(int n);
 size_t gp64_lds_bytes(int n, int np, int nw);
