@@ -360,23 +360,30 @@ def sampler_line(W: int, steps: int = 256, e2e_steps: int = 2048) -> dict:
     """Device-resident stretch move on the config-2 posterior: (1) ms per emcee
     step of rvk_stretch_run alone (proposals, priors, likelihood, accept/reject, chain into HBM;
     emcee 3's randomised split drawn on the device); (2) the wall-clock a Fitter user sees:
-    DeviceEnsembleSampler.run_mcmc of e2e_steps steps from call to return, the chain and
-    log-probs landed in host memory (emcee's get_chain arrays); next to the host stretch move
-    driving the same posterior (numpy + LogPosterior.log_probability_batch)."""
+    DeviceEnsembleSampler.run_mcmc of e2e_steps steps from call to return with the chain kept in
+    HBM (the default), then get_chain() (one copy to host memory), and the same run with the
+    chain copied to host memory chunk by chunk (chain_storage="host"); next to the host stretch
+    move driving the same posterior (numpy + LogPosterior.log_probability_batch)."""
     import torch
     from ravest_amd.sampler import DeviceEnsembleSampler, EnsembleSampler
     from ravest_amd.synth import make_posterior
     lpost, x0 = make_posterior(2, W, device=torch.cuda.current_device())
     D = x0.shape[1]
     dev_ms, acc = _stretch_raw_ms(lpost, x0, steps)
-    s = DeviceEnsembleSampler(lpost, W, seed=1234)
-    s.run_mcmc(x0, 2 * s.steps_per_call)                 # warm: buffers, pinned staging, graph capture
-    s.reset()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    s.run_mcmc(x0, e2e_steps)
-    e2e_ms = (time.perf_counter() - t0) / e2e_steps * 1e3
-    assert s.get_chain().shape == (e2e_steps, W, D)
+    e2e = {}
+    for storage in ("device", "host"):
+        s = DeviceEnsembleSampler(lpost, W, seed=1234, chain_storage=storage)
+        s.run_mcmc(x0, 2 * s.steps_per_call)             # warm: buffers, pinned staging
+        s.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.run_mcmc(x0, e2e_steps)
+        t1 = time.perf_counter()
+        chain = s.get_chain()
+        t2 = time.perf_counter()
+        assert chain.shape == (e2e_steps, W, D)
+        e2e[storage] = ((t1 - t0) / e2e_steps * 1e3, (t2 - t1) * 1e3)
+        del s, chain
     hs = EnsembleSampler(W, D, lpost.log_probability_batch, seed=1)
     hs.run_mcmc(x0, 2)
     t0 = time.perf_counter()
@@ -393,10 +400,14 @@ def sampler_line(W: int, steps: int = 256, e2e_steps: int = 2048) -> dict:
                     "Philox draws with emcee 3's randomised split, chain in HBM", "ms_per_step": dev_ms,
             "posteriors": variants,
             "walker_steps_per_s": W / (dev_ms * 1e-3), "acceptance": acc,
-            "run_mcmc_e2e_ms_per_step": e2e_ms, "run_mcmc_e2e_over_kernel": e2e_ms / dev_ms,
-            "run_mcmc_e2e_note": f"DeviceEnsembleSampler.run_mcmc of {e2e_steps} steps, call to return, chain + "
-                                 f"log-probs in host memory ({s.steps_per_call}-step chunks copied out on a copy "
-                                 "stream while the next chunk runs)",
+            "run_mcmc_e2e_ms_per_step": e2e["device"][0], "run_mcmc_e2e_over_kernel": e2e["device"][0] / dev_ms,
+            "get_chain_ms": e2e["device"][1],
+            "run_mcmc_e2e_host_chain_ms_per_step": e2e["host"][0],
+            "run_mcmc_e2e_host_chain_over_kernel": e2e["host"][0] / dev_ms,
+            "run_mcmc_e2e_note": f"DeviceEnsembleSampler.run_mcmc of {e2e_steps} steps, call to return: chain kept in "
+                                 "HBM (default; get_chain_ms = the one copy of the whole chain to host memory "
+                                 "afterwards) / chain_storage='host' (256-step chunks copied to host memory on a "
+                                 "copy stream while the next chunk runs)",
             "host_stretch_move_ms_per_step": host_ms, "speedup_vs_host": host_ms / dev_ms}
 
 

@@ -184,13 +184,14 @@ class ShardedDeviceSampler(_DevicePipeline):
     gathered block, so all ranks raise together.  (On one GPU DeviceEnsembleSampler is faster:
     one fused kernel per half-step instead of evaluate + update.)
 
-    ``keep_chain``: "all", or the rank that copies the chain to its host memory (the others
-    keep only the device chunk); ``get_autocorr_time`` is then computed on that rank and
-    broadcast, so call it on every rank, as ravest's convergence loop does."""
+    ``keep_chain``: "all", or the rank that stores the chain (in its HBM with the default
+    ``chain_storage``, or its host memory with "host"; the others keep only the device chunk);
+    ``get_autocorr_time`` is then computed on that rank and broadcast, so call it on every rank,
+    as ravest's convergence loop does."""
 
     def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed: int = 0, group=None,
                  randomize_split: bool = True, steps_per_call: int = 256, keep_chain="all",
-                 ops=None, device=None) -> None:
+                 ops=None, device=None, chain_storage: str = "auto") -> None:
         import torch
         import torch.distributed as dist
         if ops is None:
@@ -223,7 +224,8 @@ class ShardedDeviceSampler(_DevicePipeline):
             raise ValueError("keep_chain must be 'all' or a rank")
         self.keep_chain = keep_chain
         ops.reserve(self.chunk)
-        self._pipeline_init(device, keep_host=keep_chain == "all" or keep_chain == self.rank)
+        self._pipeline_init(device, keep_host=keep_chain == "all" or keep_chain == self.rank,
+                            chain_storage=chain_storage)
         self._nlp_local = torch.empty(self.chunk, dtype=torch.float64, device=device)
         self._nlp_all = torch.empty(H, dtype=torch.float64, device=device)
         self._nacc_steps = [None, None]       # per slot: [steps_per_call, W] acceptance counts after each step
@@ -278,7 +280,7 @@ class ShardedDeviceSampler(_DevicePipeline):
         ch = next((c for c in self._chunks if c.start < target <= c.start + c.n), None)
         if ch is None:
             raise RuntimeError("internal: no chunk record covers the requested step")
-        chain_d, lnp_d = self._dbuf[ch.slot]
+        chain_d, lnp_d = ch.bufs
         k = target - 1 - ch.start
         return chain_d[k], lnp_d[k], self._nacc_steps[ch.slot][k]
 

@@ -254,6 +254,111 @@ class _Backend:
         return v
 
 
+class _DeviceBackend(_Backend):
+    """The same backend with the chain and log-probabilities in device memory (HBM): the step
+    kernels write each chunk straight into its rows, nothing is copied during the run, and
+    ``get_value`` copies only the slice asked for.  288 GB per MI355X holds e.g. 10^5 steps of
+    4096 walkers x 14 parameters (46 GB).  Grown ahead of a run (device-to-device copy)."""
+
+    def __init__(self, nwalkers: int, ndim: int, device) -> None:
+        self.device = device
+        super().__init__(nwalkers, ndim)
+
+    def reset(self) -> None:
+        import torch
+        self.iteration = 0
+        self.accepted = np.zeros(self.nwalkers, dtype=np.int64)
+        self.chain = torch.empty((0, self.nwalkers, self.ndim), dtype=torch.float64, device=self.device)
+        self.log_prob = torch.empty((0, self.nwalkers), dtype=torch.float64, device=self.device)
+
+    def grow(self, ngrow: int) -> None:
+        import torch
+        need = self.iteration + ngrow
+        if need <= len(self.chain):
+            return
+        chain = torch.empty((need, self.nwalkers, self.ndim), dtype=torch.float64, device=self.device)
+        lnp = torch.empty((need, self.nwalkers), dtype=torch.float64, device=self.device)
+        if self.iteration:
+            chain[:self.iteration].copy_(self.chain[:self.iteration])
+            lnp[:self.iteration].copy_(self.log_prob[:self.iteration])
+        self.chain, self.log_prob = chain, lnp
+
+    def view(self, name: str, thin=1, discard=0):
+        """The device tensor of get_value's rows (no copy)."""
+        if self.iteration <= 0:
+            raise AttributeError("you must run the sampler with 'store == True' before accessing the results")
+        return getattr(self, name)[discard + thin - 1:self.iteration:thin]
+
+    def get_value(self, name: str, flat=False, thin=1, discard=0):
+        v = self.view(name, thin=thin, discard=discard).cpu().numpy()
+        if flat:
+            return v.reshape((-1,) + v.shape[2:])
+        return v
+
+
+class _DeviceState(State):
+    """A State whose coordinates and log-probabilities stay in device memory until first read
+    (the device-chain backend's rows: sample() yields one per step without a copy each)."""
+    __slots__ = ("_c", "_l")
+
+    def __init__(self, coords, log_prob, random_state=None) -> None:
+        self._c, self._l = coords, log_prob
+        self.blobs = None
+        self.random_state = random_state
+
+    @property
+    def coords(self):
+        if not isinstance(self._c, np.ndarray):
+            self._c = self._c.cpu().numpy()
+        return self._c
+
+    @coords.setter
+    def coords(self, v) -> None:
+        self._c = v
+
+    @property
+    def log_prob(self):
+        if self._l is not None and not isinstance(self._l, np.ndarray):
+            self._l = self._l.cpu().numpy()
+        return self._l
+
+    @log_prob.setter
+    def log_prob(self, v) -> None:
+        self._l = v
+
+
+def integrated_time_device(x, c=5, tol=50, quiet=False) -> np.ndarray:
+    """integrated_time on a device tensor x [n_steps, n_walkers, n_dim] (the device-chain
+    backend's rows): the same estimator -- per-walker autocovariance by zero-padded FFT
+    (torch.fft, fp64; real transforms), averaged over walkers, Sokal's window -- without copying
+    the chain to the host.  Agrees with the host restatement to rounding (tests/test_sampler.py)."""
+    import torch
+    if x.dim() != 3:
+        raise ValueError("invalid dimensions")
+    n_t, n_w, n_d = x.shape
+    n = next_pow_two(n_t)
+    f = torch.zeros((n_t, n_d), dtype=torch.float64, device=x.device)
+    per = max(1, (1 << 30) // (2 * n * n_d * 16))      # walkers per batch: ~1 GB of spectrum
+    for k0 in range(0, n_w, per):
+        xb = x[:, k0:k0 + per, :]
+        F = torch.fft.rfft(xb - xb.mean(dim=0, keepdim=True), n=2 * n, dim=0)
+        acf = torch.fft.irfft(F.real * F.real + F.imag * F.imag, n=2 * n, dim=0)[:n_t]
+        f += (acf / acf[0:1]).sum(dim=1)
+    taus = (2.0 * torch.cumsum(f / n_w, dim=0) - 1.0).cpu().numpy()
+    tau_est = np.empty(n_d)
+    for d in range(n_d):
+        tau_est[d] = taus[auto_window(taus[:, d], c), d]
+    flag = tol * tau_est > n_t
+    if np.any(flag):
+        msg = ("The chain is shorter than {0} times the integrated autocorrelation time for {1} parameter(s). "
+               "Use this estimate with caution and run a longer chain!\n").format(tol, np.sum(flag))
+        msg += "N/{0} = {1:.0f};\ntau: {2}".format(tol, n_t / tol, tau_est)
+        if not quiet:
+            raise AutocorrError(tau_est, msg)
+        logger.warning(msg)
+    return tau_est
+
+
 class _SamplerBase:
     """emcee.EnsembleSampler's accessors over a _Backend."""
 
@@ -294,7 +399,10 @@ class _SamplerBase:
         return np.swapaxes(self.get_log_prob(), 0, 1)
 
     def get_autocorr_time(self, discard=0, thin=1, **kwargs) -> np.ndarray:
-        """emcee: thin * integrated_time(get_chain(discard, thin), **kwargs)."""
+        """emcee: thin * integrated_time(get_chain(discard, thin), **kwargs) (on the device for a
+        device-chain backend)."""
+        if isinstance(self.backend, _DeviceBackend):
+            return thin * integrated_time_device(self.backend.view("chain", thin=thin, discard=discard), **kwargs)
         return thin * integrated_time(self.get_chain(discard=discard, thin=thin), **kwargs)
 
     def get_last_sample(self) -> State:
@@ -420,21 +528,28 @@ class EnsembleSampler(_SamplerBase):
 class _Chunk:
     """One chunk of device steps in flight: where it starts, its copy-out slot and events, and what
     its sampler needs to resume exactly at any step inside it."""
-    __slots__ = ("start", "n", "slot", "copied", "x0", "lp0", "nacc0", "draws", "rstate0")
+    __slots__ = ("start", "n", "slot", "copied", "bufs", "x0", "lp0", "nacc0", "draws", "rstate0")
 
 
 class _DevicePipeline(_SamplerBase):
     """emcee's EnsembleSampler.sample over chunks of device steps.  The walker state, the draws and
-    each chunk's chain stay in device memory; a finished chunk is copied to pinned host memory on
-    a copy stream while the next chunk runs, then into the backend's arrays, and its steps are
-    yielded one by one.  Subclasses provide the steps (_run_chunk), what a chunk must record to be
-    resumed inside (_begin_chunk) and the rewind to a step inside the last chunks (_settle,
-    naccepted)."""
+    each chunk's chain stay in device memory.  Chain storage "device" (the default on a GPU): the
+    chunk's kernels write into the device backend's rows and nothing is copied during the run
+    (get_chain copies what it returns; get_autocorr_time runs on the device).  "host": a finished
+    chunk is copied to pinned host memory on a copy stream while the next chunk runs, then into
+    the backend's host arrays.  Either way the chunk's steps are yielded one by one.  Subclasses
+    provide the steps (_run_chunk), what a chunk must record to be resumed inside (_begin_chunk)
+    and the rewind to a step inside the last chunks (_settle, naccepted)."""
 
-    def _pipeline_init(self, device, keep_host: bool = True) -> None:
+    def _pipeline_init(self, device, keep_host: bool = True, chain_storage: str = "auto") -> None:
         import torch
+        if chain_storage not in ("auto", "device", "host"):
+            raise ValueError("chain_storage must be 'auto', 'device' or 'host'")
         self.device = device
-        self.backend = _Backend(self.nwalkers, self.ndim)
+        self._dev_chain = chain_storage == "device" or (chain_storage == "auto" and device.type == "cuda")
+        self.chain_storage = "device" if self._dev_chain else "host"
+        self.backend = _DeviceBackend(self.nwalkers, self.ndim, device) if self._dev_chain else \
+            _Backend(self.nwalkers, self.ndim)
         self._keep_host = keep_host          # copy the chain to this process's host memory
         self._token = 0
         self._x = self._lp = None            # device state, at step self._dev_iter
@@ -444,6 +559,7 @@ class _DevicePipeline(_SamplerBase):
         self._chunks = []                    # the last chunks (the committed step lies in them)
         self._dbuf = [None, None]            # device chain / log-prob buffers, per slot
         self._stage = [None, None]           # pinned host staging, per slot
+        self._stage_status = [None, None]    # pinned status word, per slot
         self._copy_stream = None
         self._nslot = 0
         self._accepted_iter = 0              # backend.accepted is exact at this iteration
@@ -457,9 +573,15 @@ class _DevicePipeline(_SamplerBase):
         import torch
         return torch.cuda.current_stream(self.device) if self._cuda else None
 
-    def _ensure_buffers(self, slot: int) -> None:
+    def _ensure_buffers(self, slot: int, chunk_bufs: bool = True) -> None:
+        """The slot's status word; chunk_bufs: also its device chunk buffers and pinned staging."""
         import torch
-        if self._dbuf[slot] is not None:
+        if self._stage_status[slot] is None:
+            self._stage_status[slot] = (torch.empty(1, dtype=torch.int32, pin_memory=True) if self._cuda
+                                        else self._status.clone())
+        if self._cuda and self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("RVK_COPY_PRIO", "0")))
+        if self._dbuf[slot] is not None or not chunk_bufs:
             return
         n, W, D = self.steps_per_call, self.nwalkers, self.ndim
         self._dbuf[slot] = (torch.empty((n, W, D), dtype=torch.float64, device=self.device),
@@ -468,11 +590,9 @@ class _DevicePipeline(_SamplerBase):
             pin = dict(pin_memory=True)
             self._stage[slot] = (torch.empty((n, W, D), dtype=torch.float64, **pin) if self._keep_host else None,
                                  torch.empty((n, W), dtype=torch.float64, **pin) if self._keep_host else None,
-                                 torch.empty(1, dtype=torch.int32, **pin))
-            if self._copy_stream is None:
-                self._copy_stream = torch.cuda.Stream(self.device, priority=int(os.environ.get("RVK_COPY_PRIO", "0")))
+                                 None)
         else:                                 # host tensors: the device buffers are the staging
-            self._stage[slot] = (self._dbuf[slot][0], self._dbuf[slot][1], self._status)
+            self._stage[slot] = (self._dbuf[slot][0], self._dbuf[slot][1], None)
 
     def reset(self) -> None:
         self.backend.reset()
@@ -496,12 +616,13 @@ class _DevicePipeline(_SamplerBase):
         self._x_init = (self._dev_iter, self._x.clone(), self._lp.clone(), self._nacc.clone())
         self._chunks = []
 
-    def _enqueue(self, n: int) -> _Chunk:
+    def _enqueue(self, n: int, dev_store: bool = False) -> _Chunk:
+        """Launch the next n steps.  dev_store: into the device backend's rows (no copy-out)."""
         import torch
         stream = self._stream()
         slot = self._nslot % 2
         self._nslot += 1
-        self._ensure_buffers(slot)
+        self._ensure_buffers(slot, chunk_bufs=not dev_store)
         prev = next((c for c in reversed(self._chunks) if c.slot == slot), None)
         if prev is not None and prev.copied is not None:
             stream.wait_event(prev.copied)    # the slot's device buffers were being copied out
@@ -512,7 +633,12 @@ class _DevicePipeline(_SamplerBase):
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
         self._begin_chunk(ch)
-        chain_d, lnp_d = self._dbuf[slot]
+        if dev_store:
+            b = self.backend
+            chain_d, lnp_d = b.chain[ch.start:ch.start + n], b.log_prob[ch.start:ch.start + n]
+        else:
+            chain_d, lnp_d = self._dbuf[slot]
+        ch.bufs = (chain_d, lnp_d)
         if self._trace is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(stream)
@@ -528,9 +654,9 @@ class _DevicePipeline(_SamplerBase):
             computed.record(stream)
             cs = self._copy_stream
             cs.wait_event(computed)
-            sc, sl, ss = self._stage[slot]
+            sc, sl, _ = self._stage[slot] if not dev_store else (None,) * 3
             wg = int(os.environ.get("RVK_EGRESS_WG", "0"))   # experiment hook: copy with a few workgroups
-            if self._keep_host and wg:
+            if self._keep_host and wg and sc is not None:
                 from . import _lib
                 L = _lib.load()
                 _lib.check(L.rvk_copy_to_host(chain_d.data_ptr(), sc.data_ptr(), n * chain_d[0].numel() * 8, wg,
@@ -539,6 +665,7 @@ class _DevicePipeline(_SamplerBase):
                                               cs.cuda_stream))
             if os.environ.get("RVK_NO_EGRESS"):   # experiment hook: no chain copy-out (timing only)
                 sc = None
+            ss = self._stage_status[slot]
             with torch.cuda.stream(cs):
                 if self._keep_host and not wg and sc is not None:
                     sc[:n].copy_(chain_d[:n], non_blocking=True)
@@ -547,7 +674,9 @@ class _DevicePipeline(_SamplerBase):
             ch.copied = torch.cuda.Event()
             ch.copied.record(cs)
         else:                                 # host tensors: the chunk's status as it ended
-            self._stage[slot] = (chain_d, lnp_d, self._status.clone())
+            if not dev_store:
+                self._stage[slot] = (chain_d, lnp_d, None)
+            self._stage_status[slot] = self._status.clone()
         self._chunks = (self._chunks + [ch])[-3:]
         return ch
 
@@ -575,6 +704,7 @@ class _DevicePipeline(_SamplerBase):
                 self.random.set_state(rstate0)
             self._set_state(st)
         store = store and self._keep_host
+        dev_store = store and self._dev_chain
         if store:
             self.backend.grow(iterations)
         bar = _progress_bar(progress, iterations)
@@ -582,20 +712,21 @@ class _DevicePipeline(_SamplerBase):
         while True:
             nxt = None
             if done < iterations:
-                nxt = self._enqueue(min(self.steps_per_call, iterations - done))
+                nxt = self._enqueue(min(self.steps_per_call, iterations - done), dev_store)
                 done += nxt.n
             if pending is not None:
                 if pending.copied is not None:
                     pending.copied.synchronize()
                 if self._trace is not None:
                     self._trace.append(("copied", time.perf_counter()))
-                sc, sl, ss = self._stage[pending.slot]
+                sc, sl = (None, None) if dev_store else self._stage[pending.slot][:2]
+                ss = self._stage_status[pending.slot]
                 if int(ss[0]):
                     self._status.zero_()
                     raise ValueError("Probability function returned NaN")
                 b = self.backend
                 a, e = pending.start, pending.start + pending.n
-                if store:                     # multi-threaded copy out of the pinned staging
+                if store and not dev_store:   # multi-threaded copy out of the pinned staging
                     _copy(b.chain[a:e], sc[:pending.n])
                     _copy(b.log_prob[a:e], sl[:pending.n])
                 if self._trace is not None:
@@ -606,7 +737,8 @@ class _DevicePipeline(_SamplerBase):
                     b.iteration = e
                     if bar is not None:
                         bar.update(pending.n)
-                    yield (State(b.chain[e - 1], log_prob=b.log_prob[e - 1]) if store else
+                    yield (_DeviceState(b.chain[e - 1], b.log_prob[e - 1]) if dev_store else
+                           State(b.chain[e - 1], log_prob=b.log_prob[e - 1]) if store else
                            State(sc[pending.n - 1].numpy(), log_prob=sl[pending.n - 1].numpy(), copy=True)
                            if sc is not None else State(np.empty((0, self.ndim))))
                     if nxt is None:
@@ -619,7 +751,9 @@ class _DevicePipeline(_SamplerBase):
                                            "reset() call")
                     t = a + i
                     b.iteration = t + 1
-                    if store:
+                    if dev_store:
+                        state = _DeviceState(b.chain[t], b.log_prob[t])
+                    elif store:
                         state = State(b.chain[t], log_prob=b.log_prob[t])
                     elif sc is not None:
                         state = State(sc[i].numpy(), log_prob=sl[i].numpy(), copy=True)
@@ -644,9 +778,12 @@ class DeviceEnsembleSampler(_DevicePipeline):
     (``sample``, ``run_mcmc``, ``iteration``, ``get_chain``, ``get_log_prob``,
     ``get_autocorr_time``, ``acceptance_fraction``, ``get_last_sample``).
 
-    Steps run in chunks of ``steps_per_call`` on the device (state, draws and the chunk's chain
-    in HBM); each finished chunk is copied to pinned host memory on a copy stream while the next
-    chunk runs, and ``sample`` yields its steps one by one.  A consumer that stops early (ravest's
+    Steps run in chunks of ``steps_per_call`` on the device (state and draws in HBM).
+    ``chain_storage="auto"``/``"device"``: the chain is kept in HBM, written there by the step
+    kernels with no copy during the run (``get_chain`` copies what it returns,
+    ``get_autocorr_time`` runs on the device); ``"host"``: each finished chunk is copied to pinned
+    host memory on a copy stream while the next chunk runs.  ``sample`` yields the steps one by
+    one.  A consumer that stops early (ravest's
     convergence break) leaves the device up to one chunk ahead: the next call (and
     ``naccepted``) replays the chunk from its start up to ``iteration`` -- the draws depend only
     on (seed, global step), so the replay is exact and a run split over several calls is the
@@ -654,7 +791,7 @@ class DeviceEnsembleSampler(_DevicePipeline):
     before any of that chunk's steps is yielded (emcee raises at the step)."""
 
     def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed=None, rng: str = "philox",
-                 steps_per_call: int = 256, randomize_split: bool = True) -> None:
+                 steps_per_call: int = 256, randomize_split: bool = True, chain_storage: str = "auto") -> None:
         import torch
         from .gp import DeviceGPPosterior, GPLogPosterior
         from .posterior import DevicePosterior
@@ -682,7 +819,7 @@ class DeviceEnsembleSampler(_DevicePipeline):
         else:
             self.seed = int(seed) if seed is not None else int.from_bytes(os.urandom(8), "little")
         self.post.reserve(nwalkers)
-        self._pipeline_init(torch.device("cuda", torch.cuda.current_device()))
+        self._pipeline_init(torch.device("cuda", torch.cuda.current_device()), chain_storage=chain_storage)
 
     def _flags(self) -> int:
         from . import _lib

@@ -81,13 +81,14 @@ def test_ravest_convergence_loop_stops_early_on_51peg():
         assert abs(np.median(s.get_chain(discard=s.iteration // 2)[:, :, names.index("P_b")]) - 4.2308) < 0.01
 
 
-@pytest.mark.parametrize("rng", ["philox", "emcee"])
-def test_early_stop_resume_equals_one_run(rng):
+@pytest.mark.parametrize("rng,storage", [("philox", "device"), ("emcee", "device"), ("philox", "host"),
+                                         ("emcee", "host")])
+def test_early_stop_resume_equals_one_run(rng, storage):
     from ravest_amd.sampler import DeviceEnsembleSampler
     from ravest_amd.synth import make_posterior
     lpost, x0 = make_posterior(2, 64, seed=4)
     mk = lambda: DeviceEnsembleSampler(lpost, 64, seed=np.random.RandomState(9) if rng == "emcee" else 9,  # noqa: E731
-                                       rng=rng, steps_per_call=32)
+                                       rng=rng, steps_per_call=32, chain_storage=storage)
     ref = mk()
     ref.run_mcmc(x0, 150)
     part = mk()
@@ -105,6 +106,26 @@ def test_early_stop_resume_equals_one_run(rng):
     assert np.array_equal(s.get_log_prob(), ref.get_log_prob())
     assert np.array_equal(s.naccepted, ref.naccepted)
     assert ref.naccepted.sum() > 0
+    assert s.chain_storage == storage
+
+
+def test_device_chain_equals_host_chain():
+    """The HBM-resident chain (default) and the host-copied one are the same chain; the device
+    autocorrelation estimate equals the host restatement's; yielded states read back exactly."""
+    from ravest_amd.sampler import DeviceEnsembleSampler, integrated_time
+    from ravest_amd.synth import make_posterior
+    lpost, x0 = make_posterior(2, 128, seed=8)
+    d = DeviceEnsembleSampler(lpost, 128, seed=21, steps_per_call=40)
+    h = DeviceEnsembleSampler(lpost, 128, seed=21, steps_per_call=40, chain_storage="host")
+    states = [(st.coords.copy(), st.log_prob.copy()) for st in d.sample(x0, iterations=100)]
+    h.run_mcmc(x0, 100)
+    assert d.chain_storage == "device" and h.chain_storage == "host"
+    assert np.array_equal(d.get_chain(), h.get_chain()) and np.array_equal(d.get_log_prob(), h.get_log_prob())
+    assert np.array_equal(np.stack([c for c, _ in states]), h.get_chain())
+    assert np.array_equal(np.stack([lp for _, lp in states]), h.get_log_prob())
+    assert np.array_equal(d.get_chain(discard=10, thin=3, flat=True), h.get_chain(discard=10, thin=3, flat=True))
+    np.testing.assert_allclose(d.get_autocorr_time(tol=0), integrated_time(h.get_chain(), tol=0), rtol=1e-12)
+    assert np.array_equal(d.naccepted, h.naccepted)
 
 
 def test_split_runs_and_chunk_sizes_equal_one_run():

@@ -90,6 +90,15 @@ def test_integrated_time_matches_emcee():
     with pytest.raises(AutocorrError):
         integrated_time(x[:200], tol=50)
     assert np.all(np.isfinite(integrated_time(x[:200], tol=50, quiet=True)))
+    # the device-chain backend's estimator (torch real FFTs; a CPU tensor here, the GPU's HBM in use)
+    import torch
+    from ravest_amd.sampler import integrated_time_device
+    xt = torch.from_numpy(x)
+    assert np.allclose(integrated_time_device(xt, tol=0), tau, rtol=1e-12, atol=0)
+    with pytest.raises(AutocorrError):
+        integrated_time_device(xt[:200], tol=50)
+    assert np.allclose(integrated_time_device(xt[:200], tol=50, quiet=True),
+                       integrated_time(x[:200], tol=50, quiet=True), rtol=1e-12, atol=0)
 
 
 def test_chain_accessors_follow_emcee_backend():

@@ -3,7 +3,8 @@ stand-in for the device operations (tests/_toy_stretch_ops.py): the chain is bit
 chain, the exchange is the H per-proposal log-probabilities (8 bytes each) per half-step, a NaN in
 one rank's slice makes every rank raise (none hangs in a collective), keep_chain keeps the host
 chain on one rank and the autocorrelation estimate is broadcast from it, and a run stopped early
-and resumed equals an uninterrupted run."""
+and resumed equals an uninterrupted run -- with the chain kept in the host backend and in the
+"device" backend (torch tensors; on CPU here)."""
 import os
 import socket
 
@@ -27,21 +28,21 @@ def _x0():
     return np.random.default_rng(5).standard_normal((W, D)) * 0.5
 
 
-def _sampler(nan_at=None, keep="all"):
+def _sampler(nan_at=None, keep="all", storage="auto"):
     from ravest_amd.distributed import ShardedDeviceSampler
     from tests._toy_stretch_ops import ToyStretchOps
     return ShardedDeviceSampler(None, W, seed=11, steps_per_call=SPC, keep_chain=keep, ops=ToyStretchOps(D, nan_at),
-                                device=torch.device("cpu"))
+                                device=torch.device("cpu"), chain_storage=storage)
 
 
-def _worker(rank, world, port, q, mode):
+def _worker(rank, world, port, q, mode, storage="auto"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         if mode == "chain":
-            s = _sampler()
+            s = _sampler(storage=storage)
             s.run_mcmc(_x0(), STEPS)
             q.put((rank, s.get_chain(), s.get_log_prob(), s.naccepted.copy(), s.exchange_bytes_per_half_step))
         elif mode == "nan":
@@ -52,7 +53,7 @@ def _worker(rank, world, port, q, mode):
             except ValueError as e:
                 q.put((rank, str(e), s.iteration))
         elif mode == "keep":
-            s = _sampler(keep=0)
+            s = _sampler(keep=0, storage=storage)
             s.run_mcmc(_x0(), STEPS)
             tau = s.get_autocorr_time(tol=0)
             try:
@@ -65,11 +66,11 @@ def _worker(rank, world, port, q, mode):
         dist.destroy_process_group()
 
 
-def _spawn(world, mode):
+def _spawn(world, mode, storage="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, storage)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=180) for _ in procs), key=lambda r: r[0])
@@ -79,11 +80,11 @@ def _spawn(world, mode):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_chain_equals_one_rank(world):
+@pytest.mark.parametrize("world,storage", [(2, "host"), (3, "host"), (2, "device")])
+def test_sharded_chain_equals_one_rank(world, storage):
     ref = _sampler()
     ref.run_mcmc(_x0(), STEPS)
-    for rank, chain, lnp, nacc, xb in _spawn(world, "chain"):
+    for rank, chain, lnp, nacc, xb in _spawn(world, "chain", storage):
         assert np.array_equal(chain, ref.get_chain()), rank
         assert np.array_equal(lnp, ref.get_log_prob()), rank
         assert np.array_equal(nacc, ref.naccepted), rank
@@ -97,16 +98,18 @@ def test_nan_raises_on_every_rank():
     assert all(r[2] == 5 for r in res)                     # the chunk with step 7 starts at step 5
 
 
-def test_keep_chain_on_one_rank_and_broadcast_tau():
-    res = _spawn(2, "keep")
+@pytest.mark.parametrize("storage", ["host", "device"])
+def test_keep_chain_on_one_rank_and_broadcast_tau(storage):
+    res = _spawn(2, "keep", storage)
     assert res[0][1] and not res[1][1]
     assert np.array_equal(res[0][2], res[1][2]) and np.all(np.isfinite(res[0][2]))
 
 
-def test_early_stop_and_resume_equals_one_run():
+@pytest.mark.parametrize("storage", ["host", "device"])
+def test_early_stop_and_resume_equals_one_run(storage):
     ref = _sampler()
     ref.run_mcmc(_x0(), STEPS)
-    s = _sampler()
+    s = _sampler(storage=storage)
     for st in s.sample(_x0(), iterations=STEPS):
         if s.iteration == 12:                              # inside the third chunk; the fourth is in flight
             break
@@ -116,6 +119,13 @@ def test_early_stop_and_resume_equals_one_run():
     assert np.array_equal(s.get_chain(), ref.get_chain())
     assert np.array_equal(s.get_log_prob(), ref.get_log_prob())
     assert np.array_equal(s.naccepted, ref.naccepted)
+    if storage == "device":
+        from ravest_amd.sampler import _DeviceBackend, integrated_time
+        assert isinstance(s.backend, _DeviceBackend) and s.chain_storage == "device"
+        np.testing.assert_allclose(s.get_autocorr_time(tol=0), integrated_time(ref.get_chain(), tol=0),
+                                   rtol=1e-12, atol=0)
+        st = s.get_last_sample()
+        assert np.array_equal(st.coords, ref.get_chain()[-1]) and np.array_equal(st.log_prob, ref.get_log_prob()[-1])
 
 
 def _nacc_at(k):
