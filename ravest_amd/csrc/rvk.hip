@@ -709,7 +709,10 @@ thread_local std::string g_err;
 
 // Grid: one pass per block when W is small (4 walkers per block = 1 per wave);
 // for large W at most kMaxBlocks blocks, each looping over passes of <= WB walkers.
-constexpr long long kMaxBlocks = 2048;
+#ifndef RVK_LL_MAXBLOCKS
+#define RVK_LL_MAXBLOCKS 2048
+#endif
+constexpr long long kMaxBlocks = RVK_LL_MAXBLOCKS;
 
 template <int NP>
 void ll_grid(long long W, long long &blocks, int &wb, int wpb = kWavesPerBlock) {

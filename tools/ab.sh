@@ -4,7 +4,7 @@
 O=gpurun_out/${1:-ab}
 mkdir -p $O
 for rep in 1 2 3; do
-for so in build/variants/librvk_*.so; do
+for so in ${VARDIR:-build/variants}/librvk_*.so; do
   v=$(basename $so .so)
   RAVEST_AMD_LIB=$so timeout -k 10 200 python tools/kbench.py > $O/kb_${v}_$rep.log 2>&1 || echo "fail $v"
 done
