@@ -449,6 +449,21 @@ def config4_sampler_line(world: int, rank: int, backend: str, steps: int = 32) -
             "acceptance": float(s.acceptance_fraction.mean()), "n_gpus": world}
 
 
+def mfma_pmc(pmc, flop: float, mops_key: str):
+    """From a GP kernel's PMC summary: the matrix pipe's busy fraction (SQ_VALU_MFMA_BUSY_CYCLES
+    over 1024 SIMDs / GRBM_GUI_ACTIVE over 8 XCDs) and the MFMA FLOP issued (MOPS x 512) against
+    the algorithmic FLOP; None when the counters are missing or stale."""
+    if not pmc:
+        return None
+    c = pmc.get("counters_per_launch", {})
+    res = {"pmc": pmc.get("_file")}
+    if c.get("SQ_VALU_MFMA_BUSY_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
+        res["mfma_busy_frac"] = (c["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024) / (c["GRBM_GUI_ACTIVE"] / 8)
+    if c.get(mops_key):
+        res["mfma_flop_issued_over_algorithmic"] = c[mops_key] * 512 / flop
+    return res
+
+
 def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     """Config 5: batched quasi-periodic GP log-likelihood, 1 planet, 512
     epochs, 4096 walkers, fp32 factorisation (rvk_gp_loglike_device), theta/hyper resident in
@@ -501,23 +516,30 @@ def gp_line(W: int = 4096, n: int = 512, reps: int = 10) -> dict:
     o64, o32 = out64.cpu().numpy()[:k], out.cpu().numpy()[:k]
     fin = np.isfinite(ref)
     rel = lambda x: float(np.max(np.abs(x[fin] - ref[fin]) / np.abs(ref[fin]))) if fin.any() else 0.0   # noqa: E731
+    pmc32, pmc64 = load_pmc_file("pmc_config5.json"), load_pmc_file("pmc_config5_fp64.json")
     return {"config": f"config 5: 1 planet + quasi-periodic GP, {n} epochs, {W} walkers, fp32 factorisation",
             "ms_per_eval": ms, "walker_evals_per_s": W / (ms * 1e-3),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                          "frac": tf / FP32_MFMA_PEAK_TF,
-                         "traffic": (load_pmc_file("pmc_config5.json") or {}).get("fabric_bytes_per_launch"),
-                         "pmc": pmc_provenance("pmc_config5.json"),
+                         "traffic": (pmc32 or {}).get("fabric_bytes_per_launch"),
+                         "pmc": pmc_provenance("pmc_config5.json"), "mfma_counters": mfma_pmc(pmc32, flop,
+                                                                                          "SQ_INSTS_VALU_MFMA_MOPS_F32"),
                          "note": "algorithmic FLOP = W*(n^3/3 + 2n^2) per launch / launch duration; traffic = "
                                  "L2 memory-side (fabric) bytes per launch, FETCH_SIZE x 2 + WRITE_SIZE as "
                                  "MI355X_MICROARCH.md prescribes (PMC, profiles/pmc_config5.json): it counts "
                                  "Infinity-Cache hits too -- the workspace tiles re-read by the left-looking "
                                  "update -- so it bounds HBM bytes from above"},
             "n_masked_walkers": int((~np.isfinite(out.cpu().numpy())).sum()),
-            "precision": "fp32 factorisation, fp64 re-evaluation of walkers it rejects (default)",
+            "precision": "fp32 factorisation, fp64 re-evaluation of walkers it rejects (opt-in: precision='fp32+fp64'; "
+                         "the drop-in's default is fp64, the 'fp64' entry)",
             "max_rel_err_vs_fp64_oracle": rel(o32),
-            "fp64": {"ms_per_eval": ms64, "walker_evals_per_s": W / (ms64 * 1e-3),
+            "fp64": {"precision": "fp64 factorisation (the default: the reference's precision)",
+                     "ms_per_eval": ms64, "walker_evals_per_s": W / (ms64 * 1e-3),
                      "roofline": {"bound": "mfma", "achieved": tf64, "peak": FP64_MATRIX_PEAK_TF, "unit": "TFLOP/s",
-                                  "frac": tf64 / FP64_MATRIX_PEAK_TF},
+                                  "frac": tf64 / FP64_MATRIX_PEAK_TF,
+                                  "traffic": (pmc64 or {}).get("fabric_bytes_per_launch"),
+                                  "pmc": pmc_provenance("pmc_config5_fp64.json"),
+                                  "mfma_counters": mfma_pmc(pmc64, flop, "SQ_INSTS_VALU_MFMA_MOPS_F64")},
                      "max_rel_err_vs_fp64_oracle": rel(o64),
                      "mask_identical": bool(np.array_equal(np.isfinite(o64), fin))},
             "cpu_baseline": {"value": 1.0 / cpu_s, "unit": "walker evals/s", "cores": 1, "kind": "port",
