@@ -428,8 +428,6 @@ def config4_sampler_line(world: int, rank: int, backend: str, steps: int = 32) -
         return {"what": f"config-4 posterior, {W} walkers, {D} free parameters, 1 GPU, rvk_stretch_run (chain in HBM)",
                 "ms_per_step": ms, "walker_steps_per_s": W / (ms * 1e-3),
                 "kepler_solves_per_s": W * 512 * 2 / (ms * 1e-3), "acceptance": acc}
-    if backend != "nccl":
-        return {"skipped": "gloo rehearsal: the sharded sampler's exchange is timed with RCCL only"}
     from ravest_amd.distributed import ShardedDeviceSampler
     s = ShardedDeviceSampler(lpost, W, seed=1234, steps_per_call=steps, keep_chain=0)
     s.run_mcmc(x0, 4)
@@ -440,11 +438,12 @@ def config4_sampler_line(world: int, rank: int, backend: str, steps: int = 32) -
     torch.cuda.synchronize()
     dist.barrier()
     el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    t = torch.tensor([el], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms = float(t[0]) / steps * 1e3
-    return {"what": f"config-4 posterior, {W} walkers, {D} free parameters, ShardedDeviceSampler over {world} GPUs "
-                    f"(RCCL all-gather of {W // 2} log-probs per half-step = {s.exchange_bytes_per_half_step} B)",
+    how = "RCCL all-gather" if backend == "nccl" else f"{backend} all-gather through host memory (rehearsal, not a GPU number)"
+    return {"what": f"config-4 posterior, {W} walkers, {D} free parameters, ShardedDeviceSampler over {world} ranks "
+                    f"({how} of {W // 2} log-probs per half-step = {s.exchange_bytes_per_half_step} B)",
             "ms_per_step": ms, "walker_steps_per_s": W / (ms * 1e-3), "kepler_solves_per_s": W * 512 * 2 / (ms * 1e-3),
             "acceptance": float(s.acceptance_fraction.mean()), "n_gpus": world}
 
