@@ -64,6 +64,14 @@ def test_gp_condition_oracle_interpolates():
     mu = gp_oracle.gp_condition(ds.time, ds.vel, err, ds.inst_idx, 1, 1, 0, ds.t0, th, hy, ds.time)
     resid = ds.vel - gp_oracle.mean_model(ds.time, ds.inst_idx, 1, 1, 0, ds.t0, th[0])
     assert np.max(np.abs(mu[0] - resid)) < 1e-3 * np.max(np.abs(resid))
+    # linear in the residuals: vel -> vel + d adds the conditional mean of d alone
+    d = np.random.default_rng(9).normal(0, 3, ds.time.size)
+    tq = np.linspace(ds.time.min(), ds.time.max(), 25)
+    m = gp_oracle.mean_model(ds.time, ds.inst_idx, 1, 1, 0, ds.t0, th[0])
+    mu_v = gp_oracle.gp_condition(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:1], hy[:1], tq)[0]
+    mu_d = gp_oracle.gp_condition(ds.time, m + d, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:1], hy[:1], tq)[0]
+    mu_s = gp_oracle.gp_condition(ds.time, ds.vel + d, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[:1], hy[:1], tq)[0]
+    assert np.max(np.abs(mu_s - (mu_v + mu_d))) <= 1e-9 * np.max(np.abs(mu_s))
 
 
 class _PP:

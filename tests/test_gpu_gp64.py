@@ -337,3 +337,37 @@ def test_gp_condition_above_the_fp32_limit():
     assert np.array_equal(np.isnan(got).all(axis=1), ~ok)
     scale = np.max(np.abs(ref[ok]), axis=1, keepdims=True)
     assert np.all(np.abs(got[ok] - ref[ok]) <= 1e-8 * scale)
+
+
+def test_gp_condition_analytic_properties_device():
+    """GP conditioning on the device (RVK_GP_FP64 COND kernel), checked by properties of
+    GaussianProcess.condition that need no tinygp (its parity is unpinned):
+    mu = K(tq, t) (K + diag)^-1 r is linear in the residuals r = vel - mean(theta), reproduces r
+    at the data times as the diagonal vanishes, and goes to 0 as the noise grows."""
+    from oracle import gp_oracle
+    from ravest_amd.synth import make_dataset
+    ds = make_dataset(1, 60, 1, seed=61)
+    th, hy = _walkers(ds, 3, 61, frac_invalid=0.0)
+    hy[:] = [4.0, 80.0, 0.6, 25.0]
+    m = gp_oracle.mean_model(ds.time, ds.inst_idx, 1, 1, ds.parameterisation.code, ds.t0, th[0])
+    tq = np.linspace(ds.time.min(), ds.time.max(), 50)
+    rng = np.random.default_rng(62)
+    ra, rb = rng.normal(0, 5, ds.time.size), rng.normal(0, 5, ds.time.size)
+
+    def cond(vel, velerr, thr, tq_):
+        from ravest_amd.gp import GPKernel, GPLogLikelihood
+        g = GPLogLikelihood(ds.time, vel, velerr, ds.t0, ds.instrument, ds.unique_instruments, ds.planet_letters,
+                            ds.parameterisation, GPKernel("Quasiperiodic"), precision="fp64")
+        return g.condition(thr, hy[:len(thr)], tq_)
+
+    # linearity: r_a + r_b -> mu_a + mu_b (same theta, same diagonal)
+    mua, mub, muc = (cond(m + r, ds.velerr, th[:1], tq)[0] for r in (ra, rb, ra + rb))
+    assert np.max(np.abs(muc - (mua + mub))) <= 1e-9 * np.max(np.abs(muc))
+    # interpolation: a vanishing diagonal (velerr 1e-4, jitter 0) reproduces the residuals at the data times
+    th0 = th[:1].copy()
+    th0[0, 6] = 0.0                                       # jit_HARPS
+    mu0 = cond(m + ra, np.full(ds.time.size, 1e-4), th0, ds.time)[0]
+    assert np.max(np.abs(mu0 - ra)) <= 1e-3 * np.max(np.abs(ra))
+    # noise limit: sigma = 1e6 -> mu ~ K r / sigma^2, far below the residuals
+    mu_big = cond(m + ra, np.full(ds.time.size, 1e6), th0, tq)[0]
+    assert np.max(np.abs(mu_big)) <= 1e-9 * np.max(np.abs(ra)) * ds.time.size * hy[0, 0] ** 2
