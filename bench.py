@@ -652,7 +652,9 @@ def main():
     # pre-bound).  Measured on MI355X, config 2: at K = 20 (one replay) graph 8.6-8.7 us vs
     # eager 8.9 us wall per step (eager's kernels run 0.25 us shorter, its host issue costs
     # more); at K = 200 both 7.6 us.  N > 1: one all-gather of the G steps' log-probs every G steps.
-    G = max(1, min(args.graph_steps, args.steps))
+    # N > 1: a quarter of the steps per group (the driver's K = 20: 4 groups of 5), so the
+    # all-gather of group r overlaps group r+1's launches and only the last one is exposed
+    G = max(1, min(args.graph_steps, args.steps if world == 1 else args.steps // 4))
     while args.steps % G:                            # time exactly K steps
         G -= 1
     S = max(1, args.streams)
