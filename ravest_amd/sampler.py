@@ -546,6 +546,7 @@ class _DevicePipeline(_SamplerBase):
         if chain_storage not in ("auto", "device", "host"):
             raise ValueError("chain_storage must be 'auto', 'device' or 'host'")
         self.device = device
+        self.chain_storage_requested = chain_storage
         self._dev_chain = chain_storage == "device" or (chain_storage == "auto" and device.type == "cuda")
         self.chain_storage = "device" if self._dev_chain else "host"
         self.backend = _DeviceBackend(self.nwalkers, self.ndim, device) if self._dev_chain else \
@@ -572,6 +573,34 @@ class _DevicePipeline(_SamplerBase):
     def _stream(self):
         import torch
         return torch.cuda.current_stream(self.device) if self._cuda else None
+
+    def _device_chain_fits(self, iterations: int) -> bool:
+        """Whether growing the device chain by `iterations` steps leaves headroom in device memory
+        (chain_storage="auto" only: an explicit "device" is honoured and may raise out of memory)."""
+        import torch
+        if self.chain_storage_requested != "auto" or not self._cuda:
+            return True
+        b = self.backend
+        need = max(0, b.iteration + iterations - len(b.chain)) * self.nwalkers * (self.ndim + 1) * 8
+        if need == 0:
+            return True
+        free, _ = torch.cuda.mem_get_info(self.device)
+        return need + b.iteration * self.nwalkers * (self.ndim + 1) * 8 <= 0.8 * free
+
+    def _chain_to_host(self) -> None:
+        """Move the chain to a host backend (the run goes on with chunked copy-out)."""
+        old = self.backend
+        logger.warning("the chain no longer fits in device memory: keeping it in host memory from step %d",
+                       old.iteration)
+        new = _Backend(self.nwalkers, self.ndim)
+        new.grow(old.iteration)
+        if old.iteration:
+            _copy(new.chain[:old.iteration], old.chain[:old.iteration].cpu())
+            _copy(new.log_prob[:old.iteration], old.log_prob[:old.iteration].cpu())
+        new.iteration, new.accepted = old.iteration, old.accepted
+        self.backend = new
+        self._dev_chain = False
+        self.chain_storage = "host"
 
     def _ensure_buffers(self, slot: int, chunk_bufs: bool = True) -> None:
         """The slot's status word; chunk_bufs: also its device chunk buffers and pinned staging."""
@@ -704,6 +733,8 @@ class _DevicePipeline(_SamplerBase):
                 self.random.set_state(rstate0)
             self._set_state(st)
         store = store and self._keep_host
+        if store and self._dev_chain and not self._device_chain_fits(iterations):
+            self._chain_to_host()
         dev_store = store and self._dev_chain
         if store:
             self.backend.grow(iterations)

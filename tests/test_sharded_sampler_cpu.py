@@ -132,3 +132,19 @@ def _nacc_at(k):
     r = _sampler()
     r.run_mcmc(_x0(), k)
     return r.naccepted
+
+
+def test_device_chain_moves_to_host_when_it_no_longer_fits():
+    """chain_storage="auto" keeps the chain in device memory while it fits; a run that would not
+    fit moves the chain to host memory and goes on with the chunked copy-out -- same chain."""
+    ref = _sampler()
+    ref.run_mcmc(_x0(), STEPS)
+    s = _sampler(storage="device")
+    s.run_mcmc(_x0(), 12)
+    assert s.chain_storage == "device"
+    s._device_chain_fits = lambda iterations: False
+    s.run_mcmc(None, STEPS - 12)
+    assert s.chain_storage == "host" and isinstance(s.get_chain(), np.ndarray)
+    assert np.array_equal(s.get_chain(), ref.get_chain())
+    assert np.array_equal(s.get_log_prob(), ref.get_log_prob())
+    assert np.array_equal(s.naccepted, ref.naccepted)
