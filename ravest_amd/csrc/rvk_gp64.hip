@@ -45,6 +45,10 @@ using namespace rvk;
 
 namespace {
 
+#ifndef RVK_GP64_ABLATE
+#define RVK_GP64_ABLATE 0 // timing experiments only (wrong results): 1 A tiles, 2 B tiles of the accumulation from tile j = 0,
+                          // 4 no diagonal factor, 8 no accumulation MFMAs (loads kept)
+#endif
 #ifndef RVK_GP64_TRACE
 #define RVK_GP64_TRACE 0  // timing experiments only: s_memtime per phase, first walker of block 0
 #endif
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
             for (int k = 0; k < nt; ++k) {
                 G64_MARK(k, 0);
                 __builtin_amdgcn_s_setprio(1);    // the step's critical path goes first on its SIMD
-                {
+                if (!(RVK_GP64_ABLATE & 4)) {
                     const FactorAcc fa = factor_diag((lds_d *)fb, (lds_d *)li, (lds_d *)(Lr + k * TB),
                                                      COND ? wk + tix(k, k) * TILE : nullptr, FactorAcc{quad, dpr, pexp});
                     quad = fa.quad;
@@ -382,7 +386,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         auto issue = [&](Ops &o, int hx) {
                             const int hh = hx < NSET * k ? hx : NSET * k - 1;
                             const int j = hh / NSET, part = hh % NSET;
-                            const double2 *ta = reinterpret_cast<const double2 *>(wk + tix(k + 1, j) * TILE);
+                            const double2 *ta = reinterpret_cast<const double2 *>(
+                                wk + tix(k + 1, (RVK_GP64_ABLATE & 1) ? 0 : j) * TILE);
 #pragma unroll
                             for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -391,7 +396,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                             for (int r = 0; r < R; ++r) {
                                 const int bi = wr + NA * (qo + Q0 + r);
                                 const bool live = bi >= k + 1 && bi < nt;
-                                const double2 *tb = reinterpret_cast<const double2 *>(wk + tix(live ? bi : k + 1, j) * TILE);
+                                const double2 *tb = reinterpret_cast<const double2 *>(
+                                    wk + tix(live ? bi : k + 1, (RVK_GP64_ABLATE & 2) ? 0 : j) * TILE);
 #pragma unroll
                                 for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -421,9 +427,9 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         issue(X, 0);
                         for (int hx = 0; hx < NSET * k; hx += 2) {
                             issue(Y, hx + 1);
-                            consume(X);
+                            if (!(RVK_GP64_ABLATE & 8)) consume(X);
                             issue(X, hx + 2);
-                            consume(Y);
+                            if (!(RVK_GP64_ABLATE & 8)) consume(Y);
                         }
                     };
                     pass(std::integral_constant<int, 0>{});
