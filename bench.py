@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sampler", action="store_true", help="skip the device stretch-move measurement")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer drop-in latencies")
+    ap.add_argument("--group", action="store_true",
+                    help="start the process group and take the N>1 code path (RCCL all-gathers) even at N=1")
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
     ap.add_argument("--streams", type=int, default=1, help="independent streams per graph (--launch graph)")
     ap.add_argument("--launch", choices=["eager", "graph"], default="graph",
@@ -269,7 +272,7 @@ def config_line(cfg: int, W: int | None = None, label: str | None = None) -> dic
             "logprob_agreement": agreement(ds, ds.theta, ll, 1)}
 
 
-def config4_sharded_line(world: int, rank: int, backend: str, reps: int = 20) -> dict:
+def config4_sharded_line(world: int, rank: int, backend: str, grouped: bool = False, reps: int = 20) -> dict:
     """Config 4 as BASELINE names it: 65536 walkers (2 planets x 512 epochs) split over the N
     ranks (strong scaling, 65536/N contiguous walkers each) by ShardedDevicePosterior: each rank
     launches rvk_loglike_device on its slice and the per-walker log-probs are all-gathered (RCCL
@@ -384,11 +387,8 @@ def sampler_line(W: int, steps: int = 256, e2e_steps: int = 2048) -> dict:
         assert chain.shape == (e2e_steps, W, D)
         e2e[storage] = ((t1 - t0) / e2e_steps * 1e3, (t2 - t1) * 1e3)
         del s, chain
-    hs = EnsembleSampler(W, D, lpost.log_probability_batch, seed=1)
-    hs.run_mcmc(x0, 2)
-    t0 = time.perf_counter()
-    hs.run_mcmc(x0, 20)
-    host_ms = (time.perf_counter() - t0) / 20 * 1e3
+    host = host_stretch_ms(lpost, x0)
+    host_ms = host["routed_ms_per_step"]
     variants = {}
     for name, cfg, prior, Wv in (("config2_beta_e", 2, "beta", W), ("config2_vaneylen_e", 2, "vaneylen", W),
                                  ("config3", 3, "uniform", 16384)):
@@ -408,10 +408,108 @@ def sampler_line(W: int, steps: int = 256, e2e_steps: int = 2048) -> dict:
                                  "HBM (default; get_chain_ms = the one copy of the whole chain to host memory "
                                  "afterwards) / chain_storage='host' (256-step chunks copied to host memory on a "
                                  "copy stream while the next chunk runs)",
-            "host_stretch_move_ms_per_step": host_ms, "speedup_vs_host": host_ms / dev_ms}
+            "host_stretch_move_ms_per_step": host_ms, "host_stretch_move": host,
+            "speedup_vs_host": host_ms / dev_ms}
 
 
-def config4_sampler_line(world: int, rank: int, backend: str, steps: int = 32) -> dict:
+def _med_us(fn, reps: int) -> float:
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)) * 1e6
+
+
+def host_stretch_ms(lpost, x0, steps: int = 40) -> dict:
+    """emcee's stretch move on the host (sampler.EnsembleSampler: emcee 3.1's numpy step, its
+    RandomState call order) driving the drop-in LogPosterior.log_probability_batch -- the
+    north-star integration (fit.py:1068-1075) -- ms per step, median of 3 runs, with the phases
+    split: the sampler's own numpy work (the same step over a zero log-prob) and the drop-in's
+    two calls per step; plus the same step over the round-3 route (host priors, pageable copies)."""
+    from ravest_amd.sampler import EnsembleSampler
+    W, D = x0.shape
+
+    def per_step(fn):
+        s = EnsembleSampler(W, D, fn, seed=1)
+        s.run_mcmc(x0, 2)
+        runs = []
+        for _ in range(3):
+            s.reset()
+            t0 = time.perf_counter()
+            s.run_mcmc(x0, steps)
+            runs.append((time.perf_counter() - t0) / steps * 1e3)
+        return float(np.median(runs))
+
+    eng = lpost.log_likelihood.engine
+    routed = per_step(lpost.log_probability_batch)
+    zero = per_step(lambda q: np.zeros(len(q)))
+    q = np.ascontiguousarray(x0[: W // 2])
+    call_us = _med_us(lambda: lpost.log_probability_batch(q), 200)
+    saved = lpost._route
+    lpost._route = "host"
+    eng.set_hostio("pageable")
+    old = per_step(lpost.log_probability_batch)
+    old_call_us = _med_us(lambda: lpost.log_probability_batch(q), 100)
+    lpost._route = saved
+    eng.set_hostio("auto")
+    return {"routed_ms_per_step": routed, "sampler_numpy_ms_per_step": zero,
+            "drop_in_us_per_call": call_us, "drop_in_calls_per_step": 2,
+            "round3_route_ms_per_step": old, "round3_route_us_per_call": old_call_us,
+            "note": f"{W} walkers, {W // 2} per call; routed = device priors (rvk_logpost) + RVK_HOSTIO_AUTO; "
+                    "round3 route = host numpy/scipy priors + pageable copies (route='host', RVK_HOSTIO_PAGEABLE)"}
+
+
+def host_path_line(W: int = 4096) -> dict:
+    """The host-buffer drop-in calls a ravest user makes: LogPosterior
+    .log_probability_batch at emcee's half-ensemble (W/2 walkers), the scalar
+    log_probability(dict) MAP calls O(10^3) times (fit.py:548-604), and the raw rvk_loglike of W
+    walkers, per RVK_OPT_HOSTIO transport (median us per call); and a Powell MAP on the 51 Peg
+    golden (ravest's find_map_estimate: scipy.optimize.minimize(method="Powell") over
+    _negative_log_probability_for_MAP)."""
+    from scipy.optimize import minimize
+
+    from ravest_amd import prior as P
+    from ravest_amd.param import Parameterisation
+    from ravest_amd.posterior import LogPosterior
+    from ravest_amd.synth import make_posterior
+    lpost, x0 = make_posterior(2, W, device=0)
+    eng = lpost.log_likelihood.engine
+    H = W // 2
+    q = np.ascontiguousarray(x0[:H])
+    d1 = dict(zip(lpost.free_params_names, x0[0]))
+    full = np.ascontiguousarray(lpost._full(x0))
+    res = {}
+    for mode in ("pageable", "pinned", "zerocopy", "auto"):
+        eng.set_hostio(mode)
+        res[mode] = {"log_probability_batch_H_us": _med_us(lambda: lpost.log_probability_batch(q), 200),
+                     "log_probability_dict_us": _med_us(lambda: lpost.log_probability(d1), 400),
+                     "rvk_loglike_W_us": _med_us(lambda: eng.loglike(full), 200)}
+    eng.set_hostio("auto")
+    lpost._route = "host"
+    res["round3_route_host_priors"] = {"log_probability_batch_H_us": _med_us(lambda: lpost.log_probability_batch(q), 100),
+                                       "log_probability_dict_us": _med_us(lambda: lpost.log_probability(d1), 200)}
+    lpost._route = "device"
+    # Powell MAP on the reference's 51 Peg b golden posterior (tests/golden/logpost_51peg.npz)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "logpost_51peg.npz"))
+    m = json.loads(str(g["meta"]))
+    priors = {k: getattr(P, c)(**kw) for k, (c, kw) in m["priors"].items()}
+    lp51 = LogPosterior(m["planet_letters"], Parameterisation(m["parameterisation"]), priors, m["fixed"],
+                        m["free_names"], g["time"], g["vel"], g["velerr"], g["instrument"],
+                        np.array(m["unique_instruments"]), m["t0"], device=0)
+    start = g["theta_free"][np.argmax(g["log_prob"])]
+    lp51._negative_log_probability_for_MAP(start)
+    t0 = time.perf_counter()
+    r = minimize(lp51._negative_log_probability_for_MAP, start, method="Powell")
+    el = time.perf_counter() - t0
+    return {"what": f"host-buffer drop-in calls, config-2 posterior ({W} walkers, {x0.shape[1]} free parameters); "
+                    "median us per call", "per_transport": res,
+            "map_51peg_powell": {"evaluations": int(r.nfev), "seconds": el, "us_per_evaluation": el / r.nfev * 1e6,
+                                 "success": bool(r.success), "neg_log_post": float(r.fun)}}
+
+
+def config4_sampler_line(world: int, rank: int, backend: str, grouped: bool = False, steps: int = 32) -> dict:
     """Config 4 as a sampler: 65536 walkers (2 planets x 512 epochs, 14 free parameters).  N = 1:
     DeviceEnsembleSampler's kernel (rvk_stretch_run, one fused kernel per half-step); N > 1:
     ShardedDeviceSampler (each rank evaluates 32768 / N proposals per half-step, the 32768
@@ -423,7 +521,7 @@ def config4_sampler_line(world: int, rank: int, backend: str, steps: int = 32) -
     W = 65536
     lpost, x0 = make_posterior(4, W, device=torch.cuda.current_device())
     D = x0.shape[1]
-    if world == 1:
+    if not grouped:
         ms, acc = _stretch_raw_ms(lpost, x0, steps, warm=4)
         return {"what": f"config-4 posterior, {W} walkers, {D} free parameters, 1 GPU, rvk_stretch_run (chain in HBM)",
                 "ms_per_step": ms, "walker_steps_per_s": W / (ms * 1e-3),
@@ -597,7 +695,10 @@ def main():
     # RVK_BENCH_BACKEND=gloo: rehearsal of the N>1 path on a 1-GPU box (ranks share cuda:0, the
     # all-gather goes through host memory); the real multi-GPU run uses RCCL ("nccl").
     backend = os.environ.get("RVK_BENCH_BACKEND", "nccl")
-    if world > 1:
+    grouped = world > 1 or args.group        # --group: the N>1 path (collectives) on one GPU
+    if grouped:
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29541"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
@@ -654,13 +755,13 @@ def main():
     # more); at K = 200 both 7.6 us.  N > 1: one all-gather of the G steps' log-probs every G steps.
     # N > 1: a quarter of the steps per group (the driver's K = 20: 4 groups of 5), so the
     # all-gather of group r overlaps group r+1's launches and only the last one is exposed
-    G = max(1, min(args.graph_steps, args.steps if world == 1 else args.steps // 4))
+    G = max(1, min(args.graph_steps, args.steps if not grouped else max(1, args.steps // 4)))
     while args.steps % G:                            # time exactly K steps
         G -= 1
     S = max(1, args.streams)
     nset = 2                                         # two output sets: group r+1 overlaps gather r
     outs = [torch.empty(G, W, dtype=torch.float64, device=dev) for _ in range(nset)]
-    gath = [torch.empty(world * G * W, dtype=torch.float64, device=dev) for _ in range(nset)] if world > 1 else None
+    gath = [torch.empty(world * G * W, dtype=torch.float64, device=dev) for _ in range(nset)] if grouped else None
     from ravest_amd import _lib
     ll_fn = _lib.load().rvk_loglike_device
     call_args = [[(eng._h, th_d.data_ptr(), W, th_d.stride(0), outs[k][j].data_ptr(), stream.cuda_stream)
@@ -700,7 +801,7 @@ def main():
 
     works = [None] * nset
     rep_ev = []
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -715,9 +816,9 @@ def main():
         launch_group(k)
         b.record(stream)
         rep_ev.append((a, b))
-        if world > 1 and backend == "nccl":
+        if grouped and backend == "nccl":
             works[k] = dist.all_gather_into_tensor(gath[k], outs[k].view(-1), async_op=True)
-        elif world > 1:
+        elif grouped:
             hb = torch.empty(world * G * W, dtype=torch.float64)
             dist.all_gather_into_tensor(hb, outs[k].view(-1).cpu())
             gath[k].copy_(hb)
@@ -727,18 +828,18 @@ def main():
         if works[k] is not None:
             works[k].wait()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
     steps_run = done
     # average kernel duration inside the timed region: G back-to-back launches per event pair
     kern_ms = float(sum(a.elapsed_time(b) for a, b in rep_ev)) / steps_run
-    if world > 1:
+    if grouped:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
     ranks_same = None
-    if world > 1:
+    if grouped:
         # every rank's results, as gathered, against THIS rank's own single launch over all
         # world x W walkers (a different batch size, so possibly a different lane layout):
         # bitwise identical means the shard split changes nothing
@@ -801,6 +902,8 @@ def main():
             line["config4_shard"] = config_line(4, W=8192)
         if world == 1 and not args.no_sampler:
             line["sampler"] = sampler_line(W)
+        if world == 1 and not args.no_host_path:
+            line["host_path"] = host_path_line(W)
         if world == 1 and not args.no_gp:
             line["gp_config5"] = gp_line()
         if world == 1 and not args.no_predictive:
@@ -808,16 +911,20 @@ def main():
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
     if not args.no_configs:
-        c4 = config4_sharded_line(world, rank, backend)      # collective: every rank takes part
+        c4 = config4_sharded_line(world, rank, backend, grouped)   # collective: every rank takes part
         if rank == 0:
             line["config4_sharded"] = c4
     if not args.no_sampler:
-        c4s = config4_sampler_line(world, rank, backend)     # collective for N > 1
+        c4s = config4_sampler_line(world, rank, backend, grouped)  # collective for N > 1
         if rank == 0:
             line["config4_sampler"] = c4s
     if rank == 0:
+        if grouped:
+            line["process_group"] = {"backend": backend, "world_size": world,
+                                     "note": "timed loop with the N>1 path: async all-gather of each group's "
+                                             "log-probs, double-buffered"}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

@@ -112,14 +112,28 @@ int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, 
 
 /* Options. RVK_OPT_SOLVER: 0 = production solver (default), 1 = reference Halley.
  * RVK_OPT_GRAPH: 0 (default) = rvk_stretch_run issues plain stream launches;
- * 1 = it replays a cached HIP graph of 8 steps (same kernels; measured equal on
- * MI355X at 4096 walkers, kept for launch-bound hosts). */
+ * 1 = it replays a cached HIP graph of each draw block (up to 256 steps, a multiple
+ * of 8; same kernels; measured equal on MI355X at 4096 walkers, kept for
+ * launch-bound hosts). */
 #define RVK_OPT_SOLVER 1
 #define RVK_OPT_GRAPH  2
 /* RVK_OPT_LPW: lanes of a wave per walker for the log-likelihood kernel: 0 (default)
  * = chosen per launch from (walkers, epochs); 64, 32 or 16 = forced.  Fewer lanes per
  * walker share a wave's fixed costs between 2 or 4 walkers when epochs are few. */
 #define RVK_OPT_LPW    3
+/* RVK_OPT_HOSTIO: how the blocking host-buffer calls (rvk_loglike, rvk_logpost,
+ * rvk_gp_loglike, rvk_gp_logpost on this handle and the posteriors built on it) move
+ * their arrays.  Results are identical in every mode; only the latency differs.
+ *   RVK_HOSTIO_AUTO (default)  zero-copy up to 1 MB of input, pinned DMA above;
+ *   RVK_HOSTIO_PAGEABLE        async copies from / to the caller's own buffers;
+ *   RVK_HOSTIO_PINNED          one memcpy into pinned staging, one DMA each way;
+ *   RVK_HOSTIO_ZEROCOPY        memcpy into pinned staging; the kernels read their
+ *                              inputs and write their output there over PCIe. */
+#define RVK_OPT_HOSTIO 4
+#define RVK_HOSTIO_AUTO      0
+#define RVK_HOSTIO_PAGEABLE  1
+#define RVK_HOSTIO_PINNED    2
+#define RVK_HOSTIO_ZEROCOPY  3
 int rvk_set_option(rvk_handle *h, int32_t key, int32_t value);
 
 /* Stream the handle uses (hipStream_t as void*). */
@@ -128,7 +142,10 @@ int rvk_sync(rvk_handle *h);
 
 int rvk_device_count(void);
 const char *rvk_last_error(void);
-int rvk_version(void);   /* 100*major + minor */
+/* 100*major + minor.  101: rvk_stretch_run / rvk_gp_stretch_run take an int32 flags
+ * argument after step0 and rvk_stretch_half is gone (a caller built against 100 must
+ * not call them); RVK_OPT_HOSTIO added. */
+int rvk_version(void);
 
 #ifdef __cplusplus
 }

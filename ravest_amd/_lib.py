@@ -139,6 +139,37 @@ def load() -> C.CDLL:
     return L
 
 
+_fast = None
+
+
+def fast() -> C.CDLL:
+    """The per-call hot entry points (rvk_loglike, rvk_logpost, rvk_gp_logpost) bound with plain
+    integer addresses (``addr``) instead of ctypes pointer objects: a few microseconds less per
+    call on the host drop-in path, where the scalar log_probability(dict) of a MAP optimiser
+    is latency-bound.  Same library, same functions."""
+    global _fast
+    if _fast is None:
+        load()
+        F = C.CDLL(LIB_PATH)
+        vp, i64 = C.c_void_p, C.c_int64
+        for name in ("rvk_loglike", "rvk_logpost", "rvk_gp_logpost"):
+            getattr(F, name).argtypes = [vp, vp, i64, i64, vp]
+            getattr(F, name).restype = C.c_int
+        F.rvk_gp_loglike.argtypes = [vp, vp, vp, i64, i64, i64, vp]
+        F.rvk_gp_loglike.restype = C.c_int
+        _fast = F
+    return _fast
+
+
+def addr(a) -> int:
+    """Data address of a NumPy array (cheaper than ``a.ctypes.data``)."""
+    return a.__array_interface__["data"][0]
+
+
+HOSTIO = {"auto": 0, "pageable": 1, "pinned": 2, "zerocopy": 3}   # include/rvk.h RVK_HOSTIO_*
+OPT_HOSTIO = 4
+
+
 def check(rc: int) -> None:
     if rc != 0:
         msg = load().rvk_last_error().decode(errors="replace")

@@ -907,6 +907,74 @@ int rvk::grow_dev(void **p, size_t *cap, size_t need) {
     return RVK_OK;
 }
 
+// ---- host-buffer transport (rvk_internal.h HostIO, RVK_OPT_HOSTIO) ------------------------
+void rvk::HostIO::release() {
+    if (h) (void)hipHostFree(h);
+    (void)hipFree(d);
+    h = hd = d = nullptr;
+    hcap = dcap = 0;
+}
+
+static size_t io_align(size_t b) { return (b + 255) & ~size_t(255); }
+
+int rvk::HostIO::begin(int opt, hipStream_t st, int n_in, const void *const *src, const size_t *bytes,
+                       size_t out_bytes, const void **dev_in, void **dev_out) {
+    size_t total_in = 0, off[kHostIoMaxIn];
+    for (int i = 0; i < n_in; ++i) {
+        off[i] = total_in;
+        total_in += io_align(bytes[i]);
+    }
+    off_out = total_in;
+    const size_t total = total_in + io_align(out_bytes);
+    mode = opt == RVK_HOSTIO_AUTO ? (total_in <= kZeroCopyMaxBytes ? RVK_HOSTIO_ZEROCOPY : RVK_HOSTIO_PINNED) : opt;
+    if (mode != RVK_HOSTIO_ZEROCOPY) {
+        int rc = grow_dev((void **)&d, &dcap, total);
+        if (rc) return rc;
+    }
+    if (mode == RVK_HOSTIO_PAGEABLE) {
+        for (int i = 0; i < n_in; ++i) {
+            HIPCHK_SYNC(st, hipMemcpyAsync(d + off[i], src[i], bytes[i], hipMemcpyHostToDevice, st));
+            dev_in[i] = d + off[i];
+        }
+        *dev_out = d + off_out;
+        return RVK_OK;
+    }
+    if (total > hcap) {
+        if (h) HIPCHK(hipHostFree(h));
+        h = hd = nullptr;
+        hcap = 0;
+        // fine-grained (coherent) pinned memory: the kernels may read and write it in place
+        HIPCHK(hipHostMalloc((void **)&h, total, hipHostMallocCoherent | hipHostMallocMapped));
+        hcap = total;
+        void *dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, h, 0));
+        hd = (char *)dp;
+    }
+    for (int i = 0; i < n_in; ++i) std::memcpy(h + off[i], src[i], bytes[i]);
+    if (mode == RVK_HOSTIO_ZEROCOPY) {
+        for (int i = 0; i < n_in; ++i) dev_in[i] = hd + off[i];
+        *dev_out = hd + off_out;
+        return RVK_OK;
+    }
+    if (total_in) HIPCHK_SYNC(st, hipMemcpyAsync(d, h, total_in, hipMemcpyHostToDevice, st));   // one DMA
+    for (int i = 0; i < n_in; ++i) dev_in[i] = d + off[i];
+    *dev_out = d + off_out;
+    return RVK_OK;
+}
+
+int rvk::HostIO::end(hipStream_t st, void *out, size_t out_bytes) {
+    if (mode == RVK_HOSTIO_PAGEABLE) {
+        HIPCHK_SYNC(st, hipMemcpyAsync(out, d + off_out, out_bytes, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return RVK_OK;
+    }
+    if (mode == RVK_HOSTIO_PINNED)
+        HIPCHK_SYNC(st, hipMemcpyAsync(h + off_out, d + off_out, out_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(out, h + off_out, out_bytes);
+    return RVK_OK;
+}
+
 int rvk::shared_table(int device, const SC **tab) {
     static std::mutex mu;
     static SC *tabs[64] = {};
@@ -934,7 +1002,7 @@ int rvk_ll_trace_dump(unsigned long long *host) {
 }
 #endif
 
-int rvk_version(void) { return 100; }
+int rvk_version(void) { return 101; }
 
 const char *rvk_last_error(void) { return g_err.c_str(); }
 
@@ -958,6 +1026,7 @@ static void free_handle(rvk_handle *h) {
     (void)hipFree(h->d_out);
     (void)hipFree(h->d_tq);
     (void)hipFree(h->d_iq);
+    h->io.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1052,6 +1121,11 @@ int rvk_set_option(rvk_handle *h, int32_t key, int32_t value) {
         h->graph = value;
         return RVK_OK;
     }
+    if (key == RVK_OPT_HOSTIO) {
+        if (value < RVK_HOSTIO_AUTO || value > RVK_HOSTIO_ZEROCOPY) return fail(RVK_E_ARG, "unknown RVK_HOSTIO mode");
+        h->hostio = value;
+        return RVK_OK;
+    }
     return fail(RVK_E_ARG, "unknown option key");
 }
 
@@ -1096,18 +1170,17 @@ int rvk_loglike(rvk_handle *h, const double *theta, int64_t W, int64_t stride, d
     if (rc) return rc;
     if (W == 0) return RVK_OK;
     if (!theta || !out) return fail(RVK_E_ARG, "NULL host buffer");
+    if (h->n < 1) return fail(RVK_E_ARG, "model-only handle (n_epochs = 0) has no data to evaluate");
     HIPCHK(hipSetDevice(h->device));
-    size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
-    if ((rc = grow(&h->d_theta, &h->cap_theta, bt))) return rc;
-    if ((rc = grow(&h->d_out, &h->cap_out, bo))) return rc;
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(h->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
-    if ((rc = rvk_loglike_device(h, h->d_theta, W, stride, h->d_out, h->stream))) {
+    const void *src = theta, *d_theta = nullptr;
+    void *d_out = nullptr;
+    const size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
+    if ((rc = h->io.begin(h->hostio, h->stream, 1, &src, &bt, bo, &d_theta, &d_out))) return rc;
+    if ((rc = rvk_loglike_device(h, (const double *)d_theta, W, stride, (double *)d_out, h->stream))) {
         (void)hipStreamSynchronize(h->stream);
         return rc;
     }
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, h->d_out, bo, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    return RVK_OK;
+    return h->io.end(h->stream, out, bo);
 }
 
 int rvk_predict_device(rvk_handle *h, const double *d_theta, int64_t S, int64_t stride, const double *d_t,

@@ -951,7 +951,9 @@ struct rvk_gp {
     size_t lds64 = 0;
     long long w64stride = 0;     // doubles per workgroup workspace
     double *d_work64 = nullptr;
-    // host-buffer paths (rvk_gp_loglike, rvk_gp_predict): device copies kept across calls, grown on demand
+    // host-buffer paths: rvk_gp_loglike's transport (RVK_OPT_HOSTIO); rvk_gp_predict's device
+    // copies kept across calls, grown on demand
+    HostIO io;
     double *d_theta = nullptr, *d_hyper = nullptr, *d_out = nullptr, *d_tq = nullptr;
     size_t cap_theta = 0, cap_hyper = 0, cap_out = 0, cap_tq = 0;
 };
@@ -968,6 +970,7 @@ static void free_gp(rvk_gp *g) {
     (void)hipFree(g->d_hyper);
     (void)hipFree(g->d_out);
     (void)hipFree(g->d_tq);
+    g->io.release();
     delete g;
 }
 
@@ -1109,20 +1112,18 @@ int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t 
     rvk_handle *h = g->h;
     if (stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad walker block shape");
     HIPCHK(hipSetDevice(h->device));
-    const size_t bt = sizeof(double) * (size_t)W * (size_t)stride, bh = sizeof(double) * (size_t)W * (size_t)hstride;
+    const size_t b[2] = {sizeof(double) * (size_t)W * (size_t)stride, sizeof(double) * (size_t)W * (size_t)hstride};
+    const size_t bo = sizeof(double) * (size_t)W;
+    const void *src[2] = {theta, hyper}, *d_in[2] = {nullptr, nullptr};
+    void *d_out = nullptr;
     int rc;
-    if ((rc = gp_grow(&g->d_theta, &g->cap_theta, bt)) || (rc = gp_grow(&g->d_hyper, &g->cap_hyper, bh)) ||
-        (rc = gp_grow(&g->d_out, &g->cap_out, sizeof(double) * (size_t)W)))
-        return rc;
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_theta, theta, bt, hipMemcpyHostToDevice, h->stream));
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(g->d_hyper, hyper, bh, hipMemcpyHostToDevice, h->stream));
-    if ((rc = rvk_gp_loglike_device(g, g->d_theta, g->d_hyper, W, stride, hstride, g->d_out, h->stream))) {
+    if ((rc = g->io.begin(h->hostio, h->stream, 2, src, b, bo, d_in, &d_out))) return rc;
+    if ((rc = rvk_gp_loglike_device(g, (const double *)d_in[0], (const double *)d_in[1], W, stride, hstride,
+                                     (double *)d_out, h->stream))) {
         (void)hipStreamSynchronize(h->stream);
         return rc;
     }
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, g->d_out, sizeof(double) * (size_t)W, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    return RVK_OK;
+    return g->io.end(h->stream, out, bo);
 }
 
 int rvk_gp_predict_device(rvk_gp *g, const double *d_theta, const double *d_hyper, int64_t S, int64_t stride,
@@ -1189,8 +1190,7 @@ struct rvk_gp_post {
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;
     DrawTable tab;                 // the draws of a block of steps
-    double *d_xin = nullptr, *d_oin = nullptr;                     // rvk_gp_logpost's staging
-    size_t cap_xin = 0, cap_oin = 0;
+    HostIO io;                     // rvk_gp_logpost's host-buffer transport (RVK_OPT_HOSTIO)
 
     PostDev dev() const {
         const rvk_handle *h = g->h;
@@ -1207,8 +1207,7 @@ static void free_gp_post(rvk_gp_post *p) {
     (void)hipFree(p->d_full);
     (void)hipFree(p->d_lp);
     (void)hipFree(p->d_lhp);
-    (void)hipFree(p->d_xin);
-    (void)hipFree(p->d_oin);
+    p->io.release();
     (void)hipFree(p->d_q);
     (void)hipFree(p->d_fac);
     (void)hipFree(p->d_lau);
@@ -1353,17 +1352,15 @@ int rvk_gp_logpost(rvk_gp_post *p, const double *xf, int64_t W, int64_t stride, 
     rvk_handle *h = p->g->h;
     HIPCHK(hipSetDevice(h->device));
     const size_t bx = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
+    const void *src = xf, *d_x = nullptr;
+    void *d_out = nullptr;
     int rc;
-    if ((rc = grow_dev((void **)&p->d_xin, &p->cap_xin, bx)) || (rc = grow_dev((void **)&p->d_oin, &p->cap_oin, bo)))
-        return rc;
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(p->d_xin, xf, bx, hipMemcpyHostToDevice, h->stream));
-    if ((rc = rvk_gp_logpost_device(p, p->d_xin, W, stride, p->d_oin, h->stream))) {
+    if ((rc = p->io.begin(h->hostio, h->stream, 1, &src, &bx, bo, &d_x, &d_out))) return rc;
+    if ((rc = rvk_gp_logpost_device(p, (const double *)d_x, W, stride, (double *)d_out, h->stream))) {
         (void)hipStreamSynchronize(h->stream);
         return rc;
     }
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, p->d_oin, bo, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    return RVK_OK;
+    return p->io.end(h->stream, out, bo);
 }
 
 int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t W, int32_t n_steps, double a, uint64_t seed,

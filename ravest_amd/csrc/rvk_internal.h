@@ -55,6 +55,35 @@ int grow_dev(void **p, size_t *cap, size_t need);
 // Per-device copy of the sin/cos table, uploaded once per process (never freed).
 int shared_table(int device, const SC **tab);
 
+// Host-buffer transport of the blocking entry points (rvk_loglike, rvk_logpost, rvk_gp_logpost,
+// rvk_gp_loglike; RVK_OPT_HOSTIO).  One call: up to kHostIoMaxIn caller input buffers and one
+// output buffer.  Modes:
+//   RVK_HOSTIO_PAGEABLE  hipMemcpyAsync straight from / to the caller's (pageable) buffers;
+//   RVK_HOSTIO_PINNED    one memcpy into a pinned staging buffer, ONE DMA of all inputs into a
+//                        device buffer of the same layout, the kernels, one DMA of the output back;
+//   RVK_HOSTIO_ZEROCOPY  memcpy into the (fine-grained, device-visible) pinned staging buffer and
+//                        the kernels read their inputs from it and write their output into it
+//                        over PCIe -- no copy engine on the call's path;
+//   RVK_HOSTIO_AUTO      zero-copy up to kZeroCopyMaxBytes of input, pinned DMA above.
+// Staging and device buffers belong to the owning object and grow on demand.
+constexpr int kHostIoMaxIn = 2;
+constexpr size_t kZeroCopyMaxBytes = size_t(1) << 20;
+struct HostIO {
+    char *h = nullptr;          // pinned staging (hipHostMallocCoherent)
+    char *hd = nullptr;         // its device-visible address
+    size_t hcap = 0;
+    char *d = nullptr;          // device copy of the inputs and the output (PAGEABLE / PINNED)
+    size_t dcap = 0;
+    int mode = 0;               // resolved mode of the call in flight
+    size_t off_out = 0;         // output offset in h / d
+    void release();
+    // Stage the inputs; on return dev_in[i] / *dev_out are what the kernels use.
+    int begin(int opt, hipStream_t st, int n_in, const void *const *src, const size_t *bytes, size_t out_bytes,
+              const void **dev_in, void **dev_out);
+    // Wait for the stream and deliver the output into the caller's buffer.
+    int end(hipStream_t st, void *out, size_t out_bytes);
+};
+
 // Draw blocks (and the device stretch move's cached graphs) are a multiple of this many steps.
 constexpr int kStepsPerGraph = 8;
 
@@ -119,6 +148,8 @@ struct rvk_handle {
     int solver = 0;
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW
+    int hostio = RVK_HOSTIO_AUTO;            // RVK_OPT_HOSTIO, shared by the posteriors built on the handle
+    rvk::HostIO io;                          // rvk_loglike's transport
 
     rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw, n_planets}; }
     int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }

@@ -110,8 +110,7 @@ struct rvk_post {
     long long *d_sidx = nullptr;
     RunArgs *d_run = nullptr;              // rvk_stretch_run's per-chunk arguments
     DrawTable tab;                         // the draws of a block of steps (split_draws_kernel / host draws)
-    double *d_xin = nullptr, *d_oin = nullptr;   // rvk_logpost's host-buffer staging, grown on demand
-    size_t cap_xin = 0, cap_oin = 0;
+    HostIO io;                             // rvk_logpost's host-buffer transport (RVK_OPT_HOSTIO)
     hipStream_t cap = nullptr;             // capture stream
     hipGraphExec_t graph = nullptr;        // cached block of steps (draws_block_steps(H) steps)
     long long graph_H = 0;
@@ -199,8 +198,7 @@ static void free_post(rvk_post *p) {
     (void)hipFree(p->d_sidx);
     (void)hipFree(p->d_run);
     p->tab.release();
-    (void)hipFree(p->d_xin);
-    (void)hipFree(p->d_oin);
+    p->io.release();
     if (p->graph) (void)hipGraphExecDestroy(p->graph);
     if (p->cap) (void)hipStreamDestroy(p->cap);
     delete p;
@@ -390,18 +388,17 @@ int rvk_logpost(rvk_post *p, const double *xf, int64_t W, int64_t stride, double
     if (!xf || !out) return fail(RVK_E_ARG, "NULL host buffer");
     rvk_handle *h = p->h;
     HIPCHK(hipSetDevice(h->device));
+    int rc = reserve_impl(p, W);       // before staging: a failed allocation leaves nothing in flight
+    if (rc) return rc;
     const size_t bx = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
-    int rc;
-    if ((rc = grow_dev((void **)&p->d_xin, &p->cap_xin, bx)) || (rc = grow_dev((void **)&p->d_oin, &p->cap_oin, bo)))
-        return rc;
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(p->d_xin, xf, bx, hipMemcpyHostToDevice, h->stream));
-    if ((rc = rvk_logpost_device(p, p->d_xin, W, stride, p->d_oin, h->stream))) {
+    const void *src = xf, *d_x = nullptr;
+    void *d_out = nullptr;
+    if ((rc = p->io.begin(h->hostio, h->stream, 1, &src, &bx, bo, &d_x, &d_out))) return rc;
+    if ((rc = rvk_logpost_device(p, (const double *)d_x, W, stride, (double *)d_out, h->stream))) {
         (void)hipStreamSynchronize(h->stream);
         return rc;
     }
-    HIPCHK_SYNC(h->stream, hipMemcpyAsync(out, p->d_oin, bo, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    return RVK_OK;
+    return p->io.end(h->stream, out, bo);
 }
 
 int rvk_stretch_run(rvk_post *p, double *d_x, double *d_lp, int64_t W, int32_t n_steps, double a, uint64_t seed,

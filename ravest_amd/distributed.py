@@ -89,6 +89,7 @@ class ShardedDevicePosterior:
         self.group = group
         self.dist = dist
         init = dist.is_available() and dist.is_initialized()
+        self.grouped = init                       # a process group: the all-gather runs (even at world 1)
         self.world = dist.get_world_size(group) if init else 1      # no process group: one GPU
         self.rank = dist.get_rank(group) if init else 0
         self._inplace = init and dist.get_backend(group) == "nccl"   # RCCL's in-place all-gather
@@ -124,7 +125,7 @@ class ShardedDevicePosterior:
                 self.evaluate(theta[lo:hi], local[:hi - lo], stream)
         if not even:
             local[hi - lo:] = float("nan")                # padding, dropped below
-        if self.world > 1:
+        if self.grouped:
             src = local if (not even or self._inplace) else local.clone()
             self.dist.all_gather_into_tensor(gathered, src, group=self.group)
         if not even:
@@ -186,8 +187,8 @@ class ShardedDeviceSampler(_DevicePipeline):
 
     ``keep_chain``: "all", or the rank that stores the chain (in its HBM with the default
     ``chain_storage``, or its host memory with "host"; the others keep only the device chunk);
-    ``get_autocorr_time`` is then computed on that rank and broadcast, so call it on every rank,
-    as ravest's convergence loop does."""
+    ``get_autocorr_time`` is computed on that rank (rank 0 for "all") and broadcast, so call it
+    on every rank, as ravest's convergence loop does."""
 
     def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed: int = 0, group=None,
                  randomize_split: bool = True, steps_per_call: int = 256, keep_chain="all",
@@ -213,6 +214,7 @@ class ShardedDeviceSampler(_DevicePipeline):
         self.group = group
         self.dist = dist
         init = dist.is_available() and dist.is_initialized()
+        self.grouped = init                   # a process group: the collectives run (even at world 1)
         self.world = dist.get_world_size(group) if init else 1
         self.rank = dist.get_rank(group) if init else 0
         self.rccl = init and dist.get_backend(group) == "nccl"
@@ -240,7 +242,7 @@ class ShardedDeviceSampler(_DevicePipeline):
 
     def _gather(self, stream) -> None:
         import torch
-        if self.world == 1:
+        if not self.grouped:
             self._nlp_all.copy_(self._nlp_local)
         elif self.rccl:
             self.dist.all_gather_into_tensor(self._nlp_all, self._nlp_local, group=self.group)
@@ -316,20 +318,25 @@ class ShardedDeviceSampler(_DevicePipeline):
         return super().get_log_prob(flat=flat, thin=thin, discard=discard)
 
     def get_autocorr_time(self, discard=0, thin=1, **kwargs):
-        """emcee's estimate; with keep_chain = r computed on rank r and broadcast (collective)."""
+        """emcee's estimate, computed on ONE rank (keep_chain, or rank 0 with keep_chain="all") and
+        broadcast (collective: call it on every rank, as ravest's convergence loop does).  Every
+        rank then holds the same tau, so a convergence test cannot break on one rank and not on
+        another (with chain_storage="auto" one rank may keep its chain on the host and another in
+        HBM, whose FFTs round differently)."""
         import torch
-        if self.keep_chain == "all" or self.world == 1:
+        if not self.grouped:
             return super().get_autocorr_time(discard=discard, thin=thin, **kwargs)
+        src = 0 if self.keep_chain == "all" else self.keep_chain
         tau = torch.zeros(self.ndim, dtype=torch.float64, device=self.device if self.rccl else "cpu")
         err = torch.zeros(1, dtype=torch.float64, device=tau.device)
-        if self.rank == self.keep_chain:
+        if self.rank == src:
             try:
                 tau.copy_(torch.from_numpy(super().get_autocorr_time(discard=discard, thin=thin, **kwargs)))
             except Exception:
                 err.fill_(1.0)
-        self.dist.broadcast(err, self.keep_chain, group=self.group)
-        self.dist.broadcast(tau, self.keep_chain, group=self.group)
+        self.dist.broadcast(err, src, group=self.group)
+        self.dist.broadcast(tau, src, group=self.group)
         if float(err[0]):
             from .sampler import AutocorrError
-            raise AutocorrError(tau.cpu().numpy(), f"autocorrelation estimate failed on rank {self.keep_chain}")
+            raise AutocorrError(tau.cpu().numpy(), f"autocorrelation estimate failed on rank {src}")
         return tau.cpu().numpy()

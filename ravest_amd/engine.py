@@ -54,7 +54,8 @@ class RVEngine:
         if theta.shape[1] < self.p_full:
             raise ValueError(f"theta rows have {theta.shape[1]} values, need P_full={self.p_full}")
         out = np.empty(theta.shape[0], np.float64)
-        _lib.check(_lib.load().rvk_loglike(self._h, _p(theta), theta.shape[0], theta.shape[1], _p(out)))
+        if _lib.fast().rvk_loglike(self._h, _lib.addr(theta), theta.shape[0], theta.shape[1], _lib.addr(out)):
+            _lib.check(-1)
         return out
 
     # -- device path (async on the given / current torch stream) ---------------------
@@ -121,6 +122,11 @@ class RVEngine:
     def set_graph(self, on: bool) -> None:
         """RVK_OPT_GRAPH: the device stretch move replays a cached HIP graph per block of steps."""
         _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_GRAPH, int(bool(on))))
+
+    def set_hostio(self, mode: str) -> None:
+        """RVK_OPT_HOSTIO for the blocking host-buffer calls on this handle and the posteriors
+        built on it: "auto" (default), "pageable", "pinned" or "zerocopy" (include/rvk.h)."""
+        _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_HOSTIO, _lib.HOSTIO[mode]))
 
     def reserve(self, max_walkers: int) -> None:
         _lib.check(_lib.load().rvk_reserve(self._h, int(max_walkers)))

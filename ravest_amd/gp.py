@@ -32,7 +32,7 @@ import numpy as np
 
 from . import _lib
 from .param import Parameterisation, as_parameterisation, full_param_names
-from .prior import as_priors, device_params, logpdf_vec
+from .prior import _BUILTIN, as_priors, device_params, logpdf_vec
 
 SUPPORTED_KERNELS = ["Quasiperiodic"]
 HYPERPARAMS = ["gp_amp", "gp_lambda_e", "gp_lambda_p", "gp_period"]   # gp.py:37, the C-ABI hyper row order
@@ -198,7 +198,7 @@ class GPLogPosterior:
     def __init__(self, planet_letters, parameterisation, gp_kernel: GPKernel, priors: dict, hyperpriors: dict,
                  fixed_params: dict, fixed_hyperparams: dict, free_params_names: list, free_hyperparams_names: list,
                  time, vel, velerr, t0: float, instrument, unique_instruments, device: int = -1,
-                 precision: str = "fp64") -> None:
+                 precision: str = "fp64", route: str = "auto") -> None:
         from .posterior import LogPosterior, LogPrior
         self.planet_letters = planet_letters
         self.parameterisation = as_parameterisation(parameterisation)   # ravest's own object accepted
@@ -236,6 +236,10 @@ class GPLogPosterior:
                                     for k in HYPERPARAMS])
         self._hfree_idx = np.array([HYPERPARAMS.index(k) for k in self.free_hyperparams_names], dtype=np.int64)
         self.n_free = len(self.free_params_names) + len(self.free_hyperparams_names)
+        if route not in ("auto", "device", "host"):
+            raise ValueError("route must be 'auto', 'device' or 'host'")
+        self._route = route              # as LogPosterior.route: device priors when all are built-in
+        self._dpost = None
 
     def _classify_planet_case(self, letter: str) -> str:
         return self._pp._classify_planet_case(letter)
@@ -253,11 +257,37 @@ class GPLogPosterior:
         hyper[:, self._hfree_idx] = xh
         return xp, xh, hyper
 
+    @property
+    def route(self) -> str:
+        """Where the priors and hyperpriors are evaluated: "device" (DeviceGPPosterior, one host
+        round trip) when every one is a built-in prior class, else "host"."""
+        if self._route == "auto":
+            ok = all(isinstance(self._pp._priors[k], _BUILTIN) for k in self._pp._prior_order) and \
+                all(isinstance(self._hyperpriors[k], _BUILTIN) for k in self.free_hyperparams_names)
+            self._route = "device" if ok else "host"
+        return self._route
+
+    def _device(self) -> "DeviceGPPosterior":
+        if self._dpost is None:
+            self._dpost = DeviceGPPosterior(self)
+        return self._dpost
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_dpost"] = None
+        return d
+
     def log_probability_batch(self, x) -> np.ndarray:
         """Vectorised fit.py:7836-7901 over emcee's [W, D] block."""
         x = np.ascontiguousarray(np.atleast_2d(np.asarray(x, dtype=np.float64)))
         if x.shape[1] != self.n_free:
             raise ValueError(f"expected {self.n_free} free parameters and hyperparameters, got {x.shape[1]}")
+        if self.route == "device":
+            return self._device()._eval(x)
+        return self._host_batch(x)
+
+    def _host_batch(self, x: np.ndarray) -> np.ndarray:
+        """The host-prior form of log_probability_batch (custom priors; route="host")."""
         xp, xh, hyper = self._split(x)
         full = self._pp._full(xp)
         dead = np.any(full[:, self._pp._jit_idx] < 0, axis=1)                   # fit.py:7853-7856
@@ -340,15 +370,19 @@ class DeviceGPPosterior:
                                        float(gpost._logprob_prior_renorm_correction), flags)
         if not self._p:
             raise _lib.RVKError(f"rvk_gp_post_create failed: {_lib.last_error()}")
+        self._fn = _lib.fast().rvk_gp_logpost
 
     def __call__(self, x) -> np.ndarray:
         x = np.ascontiguousarray(np.atleast_2d(np.asarray(x, dtype=np.float64)))
         if x.shape[1] != self.n_free:
             raise ValueError(f"expected {self.n_free} free parameters and hyperparameters, got {x.shape[1]}")
+        return self._eval(x)
+
+    def _eval(self, x: np.ndarray) -> np.ndarray:
+        """rvk_gp_logpost on a C-contiguous float64 [W, n_free] block (checked by the caller)."""
         out = np.empty(x.shape[0])
-        dp = C.POINTER(C.c_double)
-        _lib.check(_lib.load().rvk_gp_logpost(self._p, x.ctypes.data_as(dp), x.shape[0], x.shape[1],
-                                              out.ctypes.data_as(dp)))
+        if self._fn(self._p, _lib.addr(x), x.shape[0], x.shape[1], _lib.addr(out)):
+            _lib.check(-1)
         return out
 
     def device(self, x, out, stream=None) -> None:

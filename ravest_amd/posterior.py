@@ -12,6 +12,10 @@ Entry points:
     log_prob_fn (emcee with ``parameter_names``; MAP; single-point callers);
   * ``log_probability_batch(theta_free[W, D]) -> ndarray[W]`` -- the
     vectorised drop-in (emcee ``vectorize=True``); ``__call__`` is the same.
+Both route through the device log-posterior (``DevicePosterior``: the scatter,
+jitter check, conversion, priors, likelihood and corrections in two kernels,
+one host round trip) whenever every prior is one of ravest's built-in classes;
+a custom callable prior keeps the host-side prior path (``route="host"``).
 Mask semantics follow fit.py:3461-3495 exactly: jitter < 0, a prior-side
 conversion ValueError, a non-finite log-prior, or an invalid planet give -inf.
 """
@@ -25,7 +29,7 @@ import numpy as np
 
 from . import _lib
 from .param import Parameterisation, as_parameterisation, full_param_names
-from .prior import Uniform, as_priors, device_params, logpdf_vec
+from .prior import _BUILTIN, Uniform, as_priors, device_params, logpdf_vec
 
 
 class LogLikelihood:
@@ -101,7 +105,7 @@ class LogPosterior:
 
     def __init__(self, planet_letters: list, parameterisation: Parameterisation, priors: dict,
                  fixed_params: dict, free_params_names: list, time, vel, velerr, instrument,
-                 unique_instruments, t0: float, engine=None, device: int = -1) -> None:
+                 unique_instruments, t0: float, engine=None, device: int = -1, route: str = "auto") -> None:
         self.planet_letters = planet_letters
         self.parameterisation = as_parameterisation(parameterisation)   # ravest's own object accepted
         self.priors = priors
@@ -122,6 +126,12 @@ class LogPosterior:
         (self._logprob_jacobian_correction, self._logprob_prior_renorm_correction,
          self._logprob_correction_breakdown) = self._compute_logprob_corrections()
         self._build_plan()
+        if route not in ("auto", "device", "host"):
+            raise ValueError("route must be 'auto', 'device' or 'host'")
+        # "auto": the device log-posterior when every prior has a device form and the likelihood
+        # engine is this package's (not a caller-supplied stand-in); "host": priors on the host
+        self._route = route
+        self._dpost = None
 
     # ---- constant corrections: fit.py:3306-3397 ------------------------------------------
     def _classify_planet_case(self, letter: str) -> str:
@@ -215,10 +225,32 @@ class LogPosterior:
         return lp, ok
 
     # ---- public API -----------------------------------------------------------------------
+    @property
+    def route(self) -> str:
+        """Where the priors of log_probability[_batch] are evaluated: "device" or "host"."""
+        if self._route == "auto":
+            from .engine import RVEngine
+            eng = self.log_likelihood._engine
+            ok = all(isinstance(self._priors[k], _BUILTIN) for k in self._prior_order) and \
+                (eng is None or isinstance(eng, RVEngine))
+            self._route = "device" if ok else "host"
+        return self._route
+
+    def _device(self) -> "DevicePosterior":
+        if self._dpost is None:
+            self._dpost = DevicePosterior(self)
+        return self._dpost
+
     def log_probability_batch(self, theta_free) -> np.ndarray:
         theta_free = np.ascontiguousarray(np.atleast_2d(np.asarray(theta_free, dtype=np.float64)))
         if theta_free.shape[1] != len(self.free_params_names):
             raise ValueError(f"expected {len(self.free_params_names)} free parameters, got {theta_free.shape[1]}")
+        if self.route == "device":
+            return self._device()._eval(theta_free)
+        return self._host_batch(theta_free)
+
+    def _host_batch(self, theta_free: np.ndarray) -> np.ndarray:
+        """The host-prior form of log_probability_batch (custom priors; route="host")."""
         full = self._full(theta_free)
         dead = np.any(full[:, self._jit_idx] < 0, axis=1)                 # fit.py:3465-3468
         lp, conv_ok = self._log_prior_batch(theta_free, full)             # fit.py:3475-3480
@@ -238,7 +270,14 @@ class LogPosterior:
 
     def log_probability(self, free_params_dict: Dict[str, float]) -> float:
         row = np.array([[free_params_dict[n] for n in self.free_params_names]], dtype=np.float64)
-        return float(self.log_probability_batch(row)[0])
+        if self.route == "device":
+            return float(self._device()._eval(row)[0])
+        return float(self._host_batch(row)[0])
+
+    def __getstate__(self):           # picklable (multiprocessing pools): device objects rebuilt lazily
+        d = dict(self.__dict__)
+        d["_dpost"] = None
+        return d
 
     def _convert_params_for_prior_evaluation(self, free_params_dict: Dict[str, float]) -> Dict[str, float]:
         """fit.py:3399-3446 (scalar form, kept for API parity)."""
@@ -314,15 +353,19 @@ class DevicePosterior:
                                     float(lpost._logprob_prior_renorm_correction), flags)
         if not self._p:
             raise _lib.RVKError(f"rvk_post_create failed: {_lib.last_error()}")
+        self._fn = _lib.fast().rvk_logpost
 
     def __call__(self, theta_free) -> np.ndarray:
         theta_free = np.ascontiguousarray(np.atleast_2d(np.asarray(theta_free, dtype=np.float64)))
         if theta_free.shape[1] != self.n_free:
             raise ValueError(f"expected {self.n_free} free parameters, got {theta_free.shape[1]}")
-        out = np.empty(theta_free.shape[0])
-        dp = C.POINTER(C.c_double)
-        _lib.check(_lib.load().rvk_logpost(self._p, theta_free.ctypes.data_as(dp), theta_free.shape[0],
-                                           theta_free.shape[1], out.ctypes.data_as(dp)))
+        return self._eval(theta_free)
+
+    def _eval(self, x: np.ndarray) -> np.ndarray:
+        """rvk_logpost on a C-contiguous float64 [W, n_free] block (checked by the caller)."""
+        out = np.empty(x.shape[0])
+        if self._fn(self._p, _lib.addr(x), x.shape[0], x.shape[1], _lib.addr(out)):
+            _lib.check(-1)
         return out
 
     def device(self, theta_free, out, stream=None) -> None:

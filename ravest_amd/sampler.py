@@ -172,17 +172,16 @@ def emcee_step_draws(random: np.random.RandomState, nwalkers: int):
                               acceptance u = random.rand() once per walker of the half
 
     Returns set[2, H] (walker indices of each half, ascending), zu[2, H],
-    rint[2, H], au[2, H]."""
+    rint[2, H], au[2, H] (indices as np.intp)."""
     W, H = nwalkers, nwalkers // 2
-    all_inds = np.arange(W)
-    inds = all_inds % 2
+    inds = np.arange(W) % 2
     random.shuffle(inds)
-    sets = np.empty((2, H), np.int32)
+    sets = np.empty((2, H), np.intp)
     zu = np.empty((2, H))
-    rint = np.empty((2, H), np.int32)
+    rint = np.empty((2, H), np.intp)
     au = np.empty((2, H))
     for split in (0, 1):
-        sets[split] = all_inds[inds == split]
+        sets[split] = np.flatnonzero(inds == split)        # all_inds[inds == split]
         zu[split] = random.rand(H)
         rint[split] = random.randint(H, size=(H,))
         au[split] = random.rand(H)            # == H successive random.rand() calls
@@ -494,33 +493,38 @@ class EnsembleSampler(_SamplerBase):
         if store:
             self.backend.grow(iterations)
         bar = _progress_bar(progress, iterations)
+        a, nd1, b = self.a, self.ndim - 1.0, self.backend
+        # emcee keeps ONE State, updates its coordinates and log-probabilities in place and yields
+        # it every step (EnsembleSampler.sample); so do we (no per-step copies of the ensemble)
+        state = State(x, log_prob=lnp)
         for _ in range(iterations):
             sets, zu, rint, au = emcee_step_draws(self.random, self.nwalkers)
             accepted = np.zeros(self.nwalkers, dtype=bool)
-            for split in (0, 1):
-                S, Cc = sets[split], sets[1 - split]
-                s, c = x[S], x[Cc]
-                zz = ((self.a - 1.0) * zu[split] + 1) ** 2.0 / self.a
-                factors = (self.ndim - 1.0) * np.log(zz)
-                q = c[rint[split]] - (c[rint[split]] - s) * zz[:, None]
+            for split in (0, 1):                               # np.take / np.compress: the same
+                S = sets[split]                                # rows as fancy indexing, ~3x faster
+                s = np.take(x, S, axis=0)
+                cr = np.take(x, np.take(sets[1 - split], rint[split]), axis=0)   # c[rint] (get_proposal)
+                zz = ((a - 1.0) * zu[split] + 1) ** 2.0 / a
+                factors = nd1 * np.log(zz)
+                q = cr - (cr - s) * zz[:, None]
                 new = np.asarray(self.log_prob_batch(q), dtype=np.float64)
-                if np.any(np.isnan(new)):
+                if np.isnan(new).any():
                     raise ValueError("Probability function returned NaN")   # emcee: -inf rejects, NaN raises
-                lnpdiff = factors + new - lnp[S]
-                acc = lnpdiff > np.log(au[split])
-                x[S[acc]] = q[acc]
-                lnp[S[acc]] = new[acc]
-                accepted[S[acc]] = True
-            b = self.backend
-            if store:
+                acc = factors + new - np.take(lnp, S) > np.log(au[split])
+                Sa = np.compress(acc, S)
+                x[Sa] = np.compress(acc, q, axis=0)
+                lnp[Sa] = np.compress(acc, new)
+                accepted[Sa] = True
+            if store:                                          # emcee's backend.save_step
                 b.chain[b.iteration] = x
                 b.log_prob[b.iteration] = lnp
-            b.accepted += accepted
-            b.iteration += 1
-            self._previous_state = State(x, log_prob=lnp, random_state=self.random.get_state(), copy=True)
+                b.accepted += accepted
+                b.iteration += 1
+            state.random_state = self.random.get_state()
+            self._previous_state = state
             if bar is not None:
                 bar.update(1)
-            yield State(x, log_prob=lnp, random_state=self.random.get_state(), copy=True)
+            yield state
         if bar is not None:
             bar.close()
 
@@ -862,7 +866,8 @@ class DeviceEnsembleSampler(_DevicePipeline):
     def _host_draws(self, n: int):
         import torch
         steps = [emcee_step_draws(self.random, self.nwalkers) for _ in range(n)]
-        return [torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in steps]))).to(self.device)
+        dt = (np.int32, np.float64, np.int32, np.float64)     # include/rvk_post.h d_set, d_zu, d_rint, d_au
+        return [torch.from_numpy(np.ascontiguousarray(np.stack([s[k] for s in steps]), dtype=dt[k])).to(self.device)
                 for k in range(4)]
 
     def _launch(self, x, lp, nacc, n, step0, draws, chain_d, lnp_d, stream) -> None:

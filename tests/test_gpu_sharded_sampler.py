@@ -59,25 +59,41 @@ def test_sharded_sampler_rejects_gp_posterior():
         ShardedDeviceSampler(gp, 16)
 
 
-def _run_ranks(tmp_path, backend, port, W=256, steps=10):
-    out = tmp_path / f"chain_{backend}.npz"
+def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2):
+    out = tmp_path / f"chain_{backend}_{nproc}.npz"
     env = dict(os.environ, RVK_TEST_BACKEND=backend, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "_sharded_sampler_worker.py"),
            str(out), str(W), str(steps)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     got = np.load(out)
+    assert int(got["world"]) == nproc
     ref = _single(W, steps)
     assert np.array_equal(got["chain"], ref.get_chain())
     assert np.array_equal(got["lnp"], ref.get_log_prob())
     assert np.array_equal(got["nacc"], ref.naccepted)
     assert int(got["xbytes"]) == (W // 2) * 8
     assert got["nacc"].sum() > 0
+    assert np.array_equal(got["tau"], ref.get_autocorr_time(tol=0))
+    for tag in ("even", "padded"):
+        if f"post_{tag}" in got.files:
+            assert np.array_equal(got[f"post_{tag}"], got[f"post_{tag}_ref"]), tag
+    return got
 
 
 def test_sharded_sampler_two_ranks_gloo(tmp_path):
     _run_ranks(tmp_path, "gloo", 29533)
+
+
+def test_rccl_world_one(tmp_path):
+    """Every RCCL branch on a one-GPU box: a world-size-1 "nccl" process group (torch.distributed.run,
+    one process) drives ShardedDeviceSampler's all-gather of the H log-posteriors (RCCL, in place on
+    device buffers), its get_autocorr_time broadcast from the chain's rank, and
+    ShardedDevicePosterior's in-place all_gather_into_tensor; chain, log-probs, acceptance counts,
+    tau and the gathered log-probs equal the single-GPU evaluation bit for bit."""
+    got = _run_ranks(tmp_path, "nccl", 29535, nproc=1)
+    assert "post_even" in got.files
 
 
 def test_sharded_sampler_two_ranks_rccl(tmp_path):
