@@ -272,7 +272,8 @@ class ShardedDeviceSampler(_DevicePipeline):
                 self.ops.update(self._x, self._lp, W, s, half, self._nlp_all, chain_d[s], lnp_d[s], prev, ns[s],
                                 self._status, stream)
             prev = ns[s]
-        self._nacc.copy_(ns[n - 1])
+        if ch.store:                          # emcee counts the acceptances of stored steps only
+            self._nacc.copy_(ns[n - 1])
 
     def _state_at(self, target: int):
         """(x, lp, nacc) device views of the state after step `target` (a step of the last chunks,
@@ -284,27 +285,27 @@ class ShardedDeviceSampler(_DevicePipeline):
             raise RuntimeError("internal: no chunk record covers the requested step")
         chain_d, lnp_d = ch.bufs
         k = target - 1 - ch.start
-        return chain_d[k], lnp_d[k], self._nacc_steps[ch.slot][k]
+        return chain_d[k], lnp_d[k], (self._nacc_steps[ch.slot][k] if ch.store else self._nacc)
 
     def _settle(self) -> None:
-        if self._x is None or self._dev_iter == self.iteration:
+        if self._x is None or self._dev_iter == self._pos:
             return
-        x, lp, nacc = self._state_at(self.iteration)
+        x, lp, nacc = self._state_at(self._pos)
         self._x.copy_(x)
         self._lp.copy_(lp)
         self._nacc.copy_(nacc)
-        self._dev_iter = self.iteration
+        self._dev_iter = self._pos
         self._chunks = []
         self._x_init = (self._dev_iter, self._x.clone(), self._lp.clone(), self._nacc.clone())
         self.backend.accepted = self._nacc.cpu().numpy()
-        self._accepted_iter = self.iteration
+        self._accepted_pos = self._pos
 
     @property
     def naccepted(self):
-        if self._accepted_iter != self.iteration:
-            src = self._nacc if self._dev_iter == self.iteration else self._state_at(self.iteration)[2]
+        if self._accepted_pos != self._pos:
+            src = self._nacc if self._dev_iter == self._pos else self._state_at(self._pos)[2]
             self.backend.accepted = src.cpu().numpy()
-            self._accepted_iter = self.iteration
+            self._accepted_pos = self._pos
         return self.backend.accepted
 
     def get_chain(self, flat=False, thin=1, discard=0):

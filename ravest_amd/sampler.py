@@ -532,7 +532,7 @@ class EnsembleSampler(_SamplerBase):
 class _Chunk:
     """One chunk of device steps in flight: where it starts, its copy-out slot and events, and what
     its sampler needs to resume exactly at any step inside it."""
-    __slots__ = ("start", "n", "slot", "copied", "bufs", "x0", "lp0", "nacc0", "draws", "rstate0")
+    __slots__ = ("start", "n", "slot", "copied", "bufs", "x0", "lp0", "nacc0", "draws", "rstate0", "row0", "store")
 
 
 class _DevicePipeline(_SamplerBase):
@@ -559,7 +559,13 @@ class _DevicePipeline(_SamplerBase):
         self._token = 0
         self._x = self._lp = None            # device state, at step self._dev_iter
         self._nacc = torch.zeros(self.nwalkers, dtype=torch.int64, device=device)
+        self._nacc_tmp = None                # acceptance counts of unstored steps (discarded, as emcee does)
         self._status = torch.zeros(1, dtype=torch.int32, device=device)
+        # Step positions: _pos = steps the consumer has taken (stored or not), _dev_iter = steps the
+        # device state has taken (up to one chunk ahead).  The draws of a step are keyed by its
+        # position, which reset() does not rewind (emcee's RandomState goes on after reset too);
+        # backend.iteration counts STORED steps only (emcee's save_step).
+        self._pos = 0
         self._dev_iter = 0
         self._chunks = []                    # the last chunks (the committed step lies in them)
         self._dbuf = [None, None]            # device chain / log-prob buffers, per slot
@@ -567,7 +573,7 @@ class _DevicePipeline(_SamplerBase):
         self._stage_status = [None, None]    # pinned status word, per slot
         self._copy_stream = None
         self._nslot = 0
-        self._accepted_iter = 0              # backend.accepted is exact at this iteration
+        self._accepted_pos = 0               # backend.accepted is exact at this position
         self._trace = [] if os.environ.get("RVK_SAMPLER_TRACE") else None   # (phase, perf_counter) timing probe
 
     @property
@@ -631,9 +637,9 @@ class _DevicePipeline(_SamplerBase):
         self.backend.reset()
         self._x = self._lp = None
         self._nacc.zero_()
-        self._dev_iter = 0
+        self._dev_iter = self._pos
         self._chunks = []
-        self._accepted_iter = 0
+        self._accepted_pos = self._pos
         self._token += 1
 
     def _set_state(self, st: State) -> None:
@@ -645,12 +651,13 @@ class _DevicePipeline(_SamplerBase):
         else:
             self._lp.copy_(torch.from_numpy(np.ascontiguousarray(st.log_prob, dtype=np.float64)))
         self._check_initial_log_prob(self._lp.cpu().numpy())
-        self._dev_iter = self.iteration
+        self._dev_iter = self._pos
         self._x_init = (self._dev_iter, self._x.clone(), self._lp.clone(), self._nacc.clone())
         self._chunks = []
 
-    def _enqueue(self, n: int, dev_store: bool = False) -> _Chunk:
-        """Launch the next n steps.  dev_store: into the device backend's rows (no copy-out)."""
+    def _enqueue(self, n: int, dev_store: bool = False, store: bool = True) -> _Chunk:
+        """Launch the next n steps.  dev_store: into the device backend's rows (no copy-out);
+        store: the steps are saved (backend rows, acceptance counts)."""
         import torch
         stream = self._stream()
         slot = self._nslot % 2
@@ -661,6 +668,9 @@ class _DevicePipeline(_SamplerBase):
             stream.wait_event(prev.copied)    # the slot's device buffers were being copied out
         ch = _Chunk()
         ch.start, ch.n, ch.slot, ch.copied = self._dev_iter, n, slot, None
+        ch.store = store
+        # backend row of the chunk's first step: rows follow the committed position
+        ch.row0 = self.backend.iteration + (self._dev_iter - self._pos) if store else None
         if self._trace is not None:
             self._trace.append(("enqueue", time.perf_counter()))
             e0 = torch.cuda.Event(enable_timing=True)
@@ -668,7 +678,7 @@ class _DevicePipeline(_SamplerBase):
         self._begin_chunk(ch)
         if dev_store:
             b = self.backend
-            chain_d, lnp_d = b.chain[ch.start:ch.start + n], b.log_prob[ch.start:ch.start + n]
+            chain_d, lnp_d = b.chain[ch.row0:ch.row0 + n], b.log_prob[ch.row0:ch.row0 + n]
         else:
             chain_d, lnp_d = self._dbuf[slot]
         ch.bufs = (chain_d, lnp_d)
@@ -747,7 +757,7 @@ class _DevicePipeline(_SamplerBase):
         while True:
             nxt = None
             if done < iterations:
-                nxt = self._enqueue(min(self.steps_per_call, iterations - done), dev_store)
+                nxt = self._enqueue(min(self.steps_per_call, iterations - done), dev_store, store)
                 done += nxt.n
             if pending is not None:
                 if pending.copied is not None:
@@ -760,7 +770,7 @@ class _DevicePipeline(_SamplerBase):
                     self._status.zero_()
                     raise ValueError("Probability function returned NaN")
                 b = self.backend
-                a, e = pending.start, pending.start + pending.n
+                a, e = pending.row0, (pending.row0 or 0) + pending.n     # backend rows (store only)
                 if store and not dev_store:   # multi-threaded copy out of the pinned staging
                     _copy(b.chain[a:e], sc[:pending.n])
                     _copy(b.log_prob[a:e], sl[:pending.n])
@@ -769,7 +779,9 @@ class _DevicePipeline(_SamplerBase):
                 if not _per_step:             # run_mcmc: the chunk's last state only
                     if tok != self._token:
                         raise RuntimeError("this run was superseded by a later sample()/run_mcmc()/reset() call")
-                    b.iteration = e
+                    self._pos = pending.start + pending.n
+                    if store:
+                        b.iteration = e
                     if bar is not None:
                         bar.update(pending.n)
                     yield (_DeviceState(b.chain[e - 1], b.log_prob[e - 1]) if dev_store else
@@ -784,8 +796,10 @@ class _DevicePipeline(_SamplerBase):
                     if tok != self._token:
                         raise RuntimeError("this sample() generator was superseded by a later sample()/run_mcmc()/"
                                            "reset() call")
-                    t = a + i
-                    b.iteration = t + 1
+                    t = (a or 0) + i
+                    self._pos = pending.start + i + 1
+                    if store:
+                        b.iteration = t + 1
                     if dev_store:
                         state = _DeviceState(b.chain[t], b.log_prob[t])
                     elif store:
@@ -886,7 +900,12 @@ class DeviceEnsembleSampler(_DevicePipeline):
         ch.draws = self._host_draws(ch.n) if self.rng == "emcee" else None
 
     def _run_chunk(self, ch: _Chunk, chain_d, lnp_d, stream) -> None:
-        self._launch(self._x, self._lp, self._nacc, ch.n, ch.start, ch.draws, chain_d, lnp_d, stream)
+        nacc = self._nacc
+        if not ch.store:                      # emcee counts the acceptances of stored steps only
+            if self._nacc_tmp is None:
+                self._nacc_tmp = self._nacc.clone()
+            nacc = self._nacc_tmp
+        self._launch(self._x, self._lp, nacc, ch.n, ch.start, ch.draws, chain_d, lnp_d, stream)
 
     def _replay_to(self, target: int, x, lp, nacc) -> None:
         """Device state of step `target` into (x, lp, nacc): from the start of the chunk that
@@ -901,31 +920,33 @@ class DeviceEnsembleSampler(_DevicePipeline):
         if k:
             draws = [t[:k] for t in ch.draws] if ch.draws else None
             self._launch(x, lp, nacc, k, ch.start, draws, None, None, self._stream())
+            if not ch.store:
+                nacc.copy_(ch.nacc0)
 
     def _settle(self) -> None:
-        """Bring the device state back to self.iteration after a generator stopped early."""
-        if self._x is None or self._dev_iter == self.iteration:
+        """Bring the device state back to the consumer's position after a generator stopped early."""
+        if self._x is None or self._dev_iter == self._pos:
             return
-        self._replay_to(self.iteration, self._x, self._lp, self._nacc)
+        self._replay_to(self._pos, self._x, self._lp, self._nacc)
         if self.rng == "emcee":
-            ch = next(c for c in self._chunks if c.start <= self.iteration <= c.start + c.n)
+            ch = next(c for c in self._chunks if c.start <= self._pos <= c.start + c.n)
             self.random.set_state(ch.rstate0)
-            for _ in range(self.iteration - ch.start):
+            for _ in range(self._pos - ch.start):
                 emcee_step_draws(self.random, self.nwalkers)
-        self._dev_iter = self.iteration
+        self._dev_iter = self._pos
         self._chunks = []
         self.backend.accepted = self._nacc.cpu().numpy()
-        self._accepted_iter = self.iteration
+        self._accepted_pos = self._pos
 
     @property
     def naccepted(self) -> np.ndarray:
-        if self._accepted_iter != self.iteration:
-            if self._dev_iter == self.iteration:
+        if self._accepted_pos != self._pos:
+            if self._dev_iter == self._pos:
                 self.backend.accepted = self._nacc.cpu().numpy()
             else:                             # a generator is suspended inside a chunk: replay on scratch
                 import torch
                 x, lp, nacc = torch.empty_like(self._x), torch.empty_like(self._lp), torch.empty_like(self._nacc)
-                self._replay_to(self.iteration, x, lp, nacc)
+                self._replay_to(self._pos, x, lp, nacc)
                 self.backend.accepted = nacc.cpu().numpy()
-            self._accepted_iter = self.iteration
+            self._accepted_pos = self._pos
         return self.backend.accepted

@@ -101,3 +101,35 @@ def test_sharded_sampler_two_ranks_rccl(tmp_path):
     if torch.cuda.device_count() < 2:
         pytest.skip("the RCCL form needs two GPUs (the driver's 8-GPU node)")
     _run_ranks(tmp_path, "nccl", 29534)
+
+
+def test_sharded_unfused_path_equals_single_gpu():
+    """P_full > 64 (1 planet, 29 instruments): the two-kernel half-step.  One GPU runs propose_kernel
+    + the 64-lane sampling kernel over the whole half; the sharded form (rvk_stretch_propose) runs
+    propose_kernel + the plain posterior kernel over its slice, whose lanes-per-walker layout is
+    chosen per launch (32 lanes at 8192 proposals).  The per-walker reduction does not depend on
+    the layout (tests/test_gpu_layout.py), so the chains are equal bit for bit."""
+    from ravest_amd import prior as P
+    from ravest_amd.distributed import ShardedDeviceSampler
+    from ravest_amd.posterior import LogPosterior
+    from ravest_amd.sampler import DeviceEnsembleSampler
+    from ravest_amd.synth import make_dataset
+    ds = make_dataset(1, 96, 29, seed=17)
+    free = [n for n in ds.names if n not in ("gd", "gdd")]
+    assert len(ds.names) > 64
+    priors = {}
+    for n in free:
+        v, base = ds.truth[n], n.split("_")[0]
+        priors[n] = (P.EccentricityUniform(0.99) if base == "e" else P.Uniform(-np.pi, np.pi) if base == "w"
+                     else P.HalfNormal(5.0) if base == "jit" else P.Uniform(v - 0.5 * abs(v) - 1.0, v + 0.5 * abs(v) + 1.0))
+    lpost = LogPosterior(ds.planet_letters, ds.parameterisation, priors, {"gd": 0.0, "gdd": 0.0}, free, ds.time,
+                         ds.vel, ds.velerr, ds.instrument, ds.unique_instruments, ds.t0)
+    W = 16384
+    rng = np.random.default_rng(3)
+    x0 = np.array([ds.truth[n] for n in free])[None, :] * (1 + 1e-4 * rng.standard_normal((W, len(free))))
+    a = DeviceEnsembleSampler(lpost, W, seed=19, steps_per_call=3)
+    a.run_mcmc(x0, 6)
+    b = ShardedDeviceSampler(lpost, W, seed=19, steps_per_call=3)
+    b.run_mcmc(x0, 6)
+    assert np.array_equal(a.get_chain(), b.get_chain()) and np.array_equal(a.get_log_prob(), b.get_log_prob())
+    assert np.array_equal(a.naccepted, b.naccepted) and a.naccepted.sum() > 0

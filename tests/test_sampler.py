@@ -155,3 +155,21 @@ def test_ravest_convergence_loop_stops_early_host():
     hist = ravest_convergence_loop(s, np.random.default_rng(1).standard_normal((32, 2)), 20000, 250, 500)
     assert s.iteration < 20000 and s.iteration in hist
     assert s.get_chain().shape[0] == s.iteration
+
+
+def test_host_sampler_store_false_semantics():
+    """emcee's save_step: store=False advances the walkers, not iteration / chain / acceptances."""
+    from ravest_amd.sampler import EnsembleSampler
+    f = lambda x: -0.5 * np.sum(x ** 2, axis=1)          # noqa: E731
+    x0 = np.random.default_rng(3).normal(size=(16, 3))
+    a = EnsembleSampler(16, 3, f, seed=7)
+    for _ in a.sample(x0, iterations=20, store=False):
+        pass
+    assert a.iteration == 0 and a.naccepted.sum() == 0
+    a.run_mcmc(None, 10)
+    b = EnsembleSampler(16, 3, f, seed=7)
+    b.run_mcmc(x0, 30)
+    assert a.iteration == 10 and np.array_equal(a.get_chain(), b.get_chain()[20:])
+    c = EnsembleSampler(16, 3, f, seed=7)
+    c.run_mcmc(x0, 20)
+    assert np.array_equal(a.naccepted, b.naccepted - c.naccepted)
