@@ -87,37 +87,47 @@ __device__ __forceinline__ int felem(int row, int col) {
     return fpair(row >> 4, kk >> 1, (col & 3) * 16 + (row & 15)) + (kk & 1);
 }
 
-__device__ __forceinline__ void park(double *tile, const Acc &a, int lane) {
-    double2 *T = reinterpret_cast<double2 *>(tile);
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-            for (int ih = 0; ih < 2; ++ih)
-                T[((p * 2 + q) * 2 + ih) * 64 + lane] = make_double2(a.c[p][q][2 * ih], a.c[p][q][2 * ih + 1]);
-}
-__device__ __forceinline__ void unpark(const double *tile, Acc &a, int lane) {
-    const double2 *T = reinterpret_cast<const double2 *>(tile);
+// park / unpark / load_frags take a global or an LDS (address_space(3)) tile pointer.
+using lds_d = __attribute__((address_space(3))) double;
+using v2d = __attribute__((ext_vector_type(2))) double;     // 16-byte pair, any address space
+using lds_v2d = __attribute__((address_space(3))) v2d;
+__device__ __forceinline__ v2d *d2p(double *p) { return reinterpret_cast<v2d *>(p); }
+__device__ __forceinline__ const v2d *d2p(const double *p) { return reinterpret_cast<const v2d *>(p); }
+__device__ __forceinline__ lds_v2d *d2p(lds_d *p) { return (lds_v2d *)p; }
+__device__ __forceinline__ const lds_v2d *d2p(const lds_d *p) { return (const lds_v2d *)p; }
+template <class P>
+__device__ __forceinline__ void park(P tile, const Acc &a, int lane) {
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
             for (int ih = 0; ih < 2; ++ih) {
-                const double2 v = T[((p * 2 + q) * 2 + ih) * 64 + lane];
+                const int o = (((p * 2 + q) * 2 + ih) * 64 + lane) * 2;
+                *d2p(tile + o) = v2d{a.c[p][q][2 * ih], a.c[p][q][2 * ih + 1]};
+            }
+}
+template <class P>
+__device__ __forceinline__ void unpark(P tile, Acc &a, int lane) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int ih = 0; ih < 2; ++ih) {
+                const v2d v = *d2p(tile + (((p * 2 + q) * 2 + ih) * 64 + lane) * 2);
                 a.c[p][q][2 * ih] = v.x;
                 a.c[p][q][2 * ih + 1] = v.y;
             }
 }
 // all 16 fragments of a fragment-layout tile: f[s][kk]
-__device__ __forceinline__ void load_frags(const double *tile, double (&f)[2][8], int lane) {
-    const double2 *T = reinterpret_cast<const double2 *>(tile);
+template <class P>
+__device__ __forceinline__ void load_frags(P tile, double (&f)[2][8], int lane) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int kk2 = 0; kk2 < 4; ++kk2) {
-            const double2 v = T[(s * 4 + kk2) * 64 + lane];
+            const v2d v = *d2p(tile + ((s * 4 + kk2) * 64 + lane) * 2);
             f[s][2 * kk2] = v.x;
             f[s][2 * kk2 + 1] = v.y;
         }
@@ -142,7 +152,6 @@ struct FactorAcc {
     double quad, dpr;
     int pexp;
 };
-using lds_d = __attribute__((address_space(3))) double;
 __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li, lds_d *Lr, double *xdiag,
                                                            FactorAcc fa) {
     const int lane = threadIdx.x & 63;
@@ -212,6 +221,91 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
     return FactorAcc{quad, dpr, pexp};
 }
 
+// ---- the accumulation of one step (row owners), software-pipelined -------------------------
+// acc(bi, k+1) -= sum_{j<k} L(bi, j) L(k+1, j)^T for the wave's live rows bi = wr + NA r, r = A..B
+// (at most 3 at a time: the B operands of every live row share one load of the A operand
+// L(k+1, j)).  The operands stream in quarter tiles (2 of the 8 k-steps of a 32 x 32 x 32
+// product: one 16-byte load per lane per fragment row) through a ring of D register sets:
+// D - 1 quarters are always in flight while one is consumed, and scheduling barriers keep the
+// compiler from sinking the loads next to their MFMAs (which left every quarter's load latency
+// exposed: the accumulation ran at ~40 % of the matrix pipe, profiles/round2/gp64_phase_trace.txt).
+#ifndef RVK_GP64_RING
+#define RVK_GP64_RING 3
+#endif
+template <int R>
+struct Ops64 {
+    double2 a[2];
+    double2 b[R][2];
+};
+
+template <int MAXR, int NA, int A, int B, int D>
+__device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, int wr, int lane) {
+    constexpr int R = B - A + 1;
+    const int NQ = 4 * k;                           // quarters (j, part), j < k
+    const double2 *rowa = reinterpret_cast<const double2 *>(wk + tix(k + 1, 0) * TILE) + lane;
+    const double2 *rowb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rowb[r] = reinterpret_cast<const double2 *>(wk + tix(wr + NA * (A + r), 0) * TILE) + lane;
+    Ops64<R> ops[D];
+    auto issue = [&](Ops64<R> &o, int hx) {         // unconditional (clamped past the end): the
+        hx = hx < NQ ? hx : NQ - 1;                 // wait counts stay exact on every path
+        const int j = hx >> 2, part = hx & 3;
+        const int off = j * (TILE / 2) + part * 64;  // double2 units: tiles of row bi are contiguous in j
+        o.a[0] = rowa[off];
+        o.a[1] = rowa[off + 256];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            o.b[r][0] = rowb[r][off];
+            o.b[r][1] = rowb[r][off + 256];
+        }
+    };
+    auto consume = [&](const Ops64<R> &o) {
+#pragma unroll
+        for (int cmp = 0; cmp < 2; ++cmp)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        acc[A + r].c[p][q] = mfma64(cmp ? o.a[p].y : o.a[p].x, cmp ? o.b[r][q].y : o.b[r][q].x,
+                                                    acc[A + r].c[p][q]);
+    };
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) issue(ops[d], d);
+    for (int hx = 0; hx < NQ; hx += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            issue(ops[(d + D - 1) % D], hx + d + D - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (hx + d < NQ) consume(ops[d]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// The live rows A0 .. B0 of a wave (a suffix of its rows: rows finish in order), in spans of <= 3.
+template <int MAXR, int NA, int D>
+__device__ __forceinline__ void accum_rows(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, int wr, int lane,
+                                           int a0, int b0) {
+    for (int a = a0; a <= b0; a += 3) {
+        const int b = a + 2 < b0 ? a + 2 : b0;
+#define RVK_SPAN(X, Y)                                                                   \
+    if constexpr (Y < MAXR) {                                                            \
+        if (a == X && b == Y) accum_span<MAXR, NA, X, Y, D>(acc, wk, k, wr, lane);       \
+    }
+        RVK_SPAN(0, 0) RVK_SPAN(0, 1) RVK_SPAN(0, 2) RVK_SPAN(1, 1) RVK_SPAN(1, 2) RVK_SPAN(1, 3)
+        RVK_SPAN(2, 2) RVK_SPAN(2, 3) RVK_SPAN(2, 4) RVK_SPAN(3, 3) RVK_SPAN(3, 4) RVK_SPAN(4, 4)
+#undef RVK_SPAN
+    }
+}
+
+#ifndef RVK_GP64_LDSPARK
+#define RVK_GP64_LDSPARK 1   // parked accumulators and S1's new tiles in LDS slots (nt <= 16)
+#endif
+template <int MAXR, bool GROUPED>
+constexpr bool gp64_ldsp() { return RVK_GP64_LDSPARK && MAXR == 3 && !GROUPED; }
+
 // MAXR tile rows per row-owning wave; GROUPED: nt > MAXR * (NW - 1), the rows go through the workspace in
 // groups of MAXR (a separate instantiation: the common shape keeps its register allocation)
 template <int NW, int MAXR, bool COND, bool GROUPED>
@@ -220,7 +314,13 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     extern __shared__ double smem64[];
     const int n = a.n, ni = a.ni, np = a.np;
     const int nt = (n + TB - 1) / TB, npad = nt * TB;
-    double *Lt = smem64;              // [npad] epochs (padding: t[n-1])
+    // LDSP (nt <= 16): every tile row bi >= 1 has an LDS slot that holds, in turn, its parked
+    // accumulator acc(bi, k) (S2(k-1) -> S1(k)) and its new factor tile L(bi, k) (S1(k) -> S2(k)),
+    // so S1 and S2 read their operands from LDS instead of the workspace (15 x 8 KB at n = 512)
+    constexpr bool LDSP = gp64_ldsp<MAXR, GROUPED>();
+    double *slots = smem64;           // [nt - 1][TILE] (LDSP)
+    auto pslot = [&](int bi) { return (lds_d *)(slots + (bi - 1) * TILE); };
+    double *Lt = smem64 + (LDSP ? (nt - 1) * TILE : 0);   // [npad] epochs (padding: t[n-1])
     double *Lr = Lt + npad;           // [npad] rhs r, reduced in place; segment k becomes y_k (then alpha_k)
     double *Ldia = Lr + npad;         // [npad] velerr^2 + jit^2 (padding: 1)
     double *fb = Ldia + npad;         // [TB][FS] the factor's row buffer; back substitution partial sums
@@ -325,6 +425,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 Acc t;
                 cov_tile(bi, 0, t);
                 if (bi == 0) put_diag(t);
+                else if constexpr (LDSP) park(pslot(bi), t, lane);
                 else park(wk + tix(bi, 0) * TILE, t, lane);
             }
         }
@@ -432,10 +533,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                             if (!(RVK_GP64_ABLATE & 8)) consume(Y);
                         }
                     };
-                    pass(std::integral_constant<int, 0>{});
-                    if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
-                    if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
-                    if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
+                    if constexpr (!grouped && RVK_GP64_RING > 1) {
+                        // the live rows (a suffix of the owned ones), software-pipelined
+                        const int r0 = k + 1 > wr ? (k + 1 - wr + NA - 1) / NA : 0;
+                        if (k > 0 && r0 < nown && !(RVK_GP64_ABLATE & 8))
+                            accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, wr, lane, r0, nown - 1);
+                    } else {
+                        pass(std::integral_constant<int, 0>{});
+                        if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
+                        if constexpr (MAXR > 4) pass(std::integral_constant<int, 4>{});
+                        if constexpr (MAXR > 6) pass(std::integral_constant<int, 6>{});
+                    }
                     if constexpr (grouped) {                // park the group: S2 reads it back
 #pragma unroll
                         for (int q = 0; q < MAXR; ++q) {
@@ -473,7 +581,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     if (bi > k && bi < nt) {
                         double *T = wk + tix(bi, k) * TILE;
                         Acc cur;
-                        unpark(T, cur, lane);
+                        if constexpr (LDSP) unpark(pslot(bi), cur, lane);
+                        else unpark(T, cur, lane);
                         Acc o;
 #pragma unroll
                         for (int p = 0; p < 2; ++p)
@@ -489,15 +598,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                                     o.c[p][qq] = mfma64(xa[p][kk], cur.c[kk >> 2][qq][kk & 3], o.c[p][qq]);
                         // o.c[p][qq][i] at lane l = L(bi, k)[16 qq + (l & 15)][16 p + (l >> 4) + 4 i]
                         //                         = frag(qq, 4 p + i)[l]
-                        double2 *T2 = reinterpret_cast<double2 *>(T);
 #pragma unroll
                         for (int qq = 0; qq < 2; ++qq) {
                             double s = 0.0;
 #pragma unroll
                             for (int p = 0; p < 2; ++p) {
 #pragma unroll
-                                for (int ih = 0; ih < 2; ++ih)
-                                    T2[(qq * 4 + 2 * p + ih) * 64 + lane] = make_double2(o.c[p][qq][2 * ih], o.c[p][qq][2 * ih + 1]);
+                                for (int ih = 0; ih < 2; ++ih) {
+                                    const v2d v = {o.c[p][qq][2 * ih], o.c[p][qq][2 * ih + 1]};
+                                    d2p(T)[(qq * 4 + 2 * p + ih) * 64 + lane] = v;
+                                    if constexpr (LDSP) d2p(pslot(bi))[(qq * 4 + 2 * p + ih) * 64 + lane] = v;   // for S2
+                                }
 #pragma unroll
                                 for (int i = 0; i < 4; ++i) s = __builtin_fma(o.c[p][qq][i], yv[p][i], s);
                             }
@@ -514,10 +625,12 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 // ---- S2(k): the j = k term; park for S1(k+1), the diagonal tile to fb -----------
             {
                 double af[2][8];
-                load_frags(wk + tix(k + 1, k) * TILE, af, lane);
+                if constexpr (LDSP) load_frags(pslot(k + 1), af, lane);
+                else load_frags(wk + tix(k + 1, k) * TILE, af, lane);
                 auto s2 = [&](Acc &acc, int bi) {
                     double bf[2][8];
-                    load_frags(wk + tix(bi, k) * TILE, bf, lane);
+                    if constexpr (LDSP) load_frags(pslot(bi), bf, lane);
+                    else load_frags(wk + tix(bi, k) * TILE, bf, lane);
 #pragma unroll
                     for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
@@ -526,6 +639,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                             for (int qq = 0; qq < 2; ++qq)
                                 acc.c[p][qq] = mfma64(af[p][kk], bf[qq][kk], acc.c[p][qq]);
                     if (bi == k + 1) put_diag(acc);
+                    else if constexpr (LDSP) park(pslot(bi), acc, lane);
                     else park(wk + tix(bi, k + 1) * TILE, acc, lane);
                 };
                 if constexpr (!grouped) {
@@ -634,6 +748,7 @@ Gp64Shape gp64_shape(int n) {
 size_t gp64_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * (3 * (size_t)nt * TB + TB * FS + TILE + 2 * (size_t)nw);
+    if (gp64_shape(n).maxr == 3 && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
     return b;
 }
