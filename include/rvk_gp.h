@@ -115,6 +115,21 @@ int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t n_walk
                        const int32_t *d_rint, const double *d_au, double *d_chain, double *d_lnp,
                        int64_t *d_naccepted, int32_t *d_status, void *stream);
 
+/* The multi-GPU form of rvk_gp_stretch_run (GPFitter.run_mcmc's pool.map over walkers,
+ * fit.py:4983-4990), with rvk_stretch_draws / _propose / _update's contract (include/rvk_post.h):
+ * every rank holds the whole ensemble and the same draws; per half-step rank r evaluates the
+ * GP log-posterior of its slice [j0, j0 + count) of the W/2 proposals (rvk_gp_stretch_propose),
+ * the W/2 log-posteriors are all-gathered (8 bytes each) and every rank applies the accept /
+ * reject to the whole half (rvk_gp_stretch_update).  The chain equals rvk_gp_stretch_run's
+ * with the same seed bit for bit. */
+int rvk_gp_stretch_draws(rvk_gp_post *p, int64_t n_walkers, int32_t n_steps, double a, uint64_t seed, uint64_t step0,
+                         int32_t flags, void *stream);
+int rvk_gp_stretch_propose(rvk_gp_post *p, const double *d_x, int64_t n_walkers, int32_t s, int32_t half, int64_t j0,
+                           int64_t count, double *d_out, void *stream);
+int rvk_gp_stretch_update(rvk_gp_post *p, double *d_x, double *d_lp, int64_t n_walkers, int32_t s, int32_t half,
+                          const double *d_nlp, double *d_chain_step, double *d_lnp_step, const int64_t *d_nacc_in,
+                          int64_t *d_nacc_out, int32_t *d_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

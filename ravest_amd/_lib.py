@@ -23,7 +23,8 @@ EXPORTS = ["rvk_create", "rvk_destroy", "rvk_loglike", "rvk_loglike_device", "rv
            "rvk_stretch_run", "rvk_stretch_draws", "rvk_stretch_propose", "rvk_stretch_update", "rvk_stretch_table_read", "rvk_copy_to_host",
            "rvk_gp_create", "rvk_gp_destroy", "rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_gp_set_precision",
            "rvk_gp_predict", "rvk_gp_predict_device", "rvk_gp_post_create", "rvk_gp_post_destroy",
-           "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device", "rvk_gp_stretch_run"]
+           "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device", "rvk_gp_stretch_run",
+           "rvk_gp_stretch_draws", "rvk_gp_stretch_propose", "rvk_gp_stretch_update"]
 
 OPT_SOLVER = 1
 OPT_GRAPH = 2
@@ -128,9 +129,13 @@ def load() -> C.CDLL:
     L.rvk_gp_logpost.argtypes = [vp, dp, C.c_int64, C.c_int64, dp]
     L.rvk_gp_logpost_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
     L.rvk_gp_stretch_run.argtypes = list(L.rvk_stretch_run.argtypes)
+    L.rvk_gp_stretch_draws.argtypes = list(L.rvk_stretch_draws.argtypes)
+    L.rvk_gp_stretch_propose.argtypes = list(L.rvk_stretch_propose.argtypes)
+    L.rvk_gp_stretch_update.argtypes = list(L.rvk_stretch_update.argtypes)
     for name in ("rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_gp_set_precision", "rvk_gp_predict",
                  "rvk_gp_predict_device", "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device",
-                 "rvk_gp_stretch_run", "rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
+                 "rvk_gp_stretch_run", "rvk_gp_stretch_draws", "rvk_gp_stretch_propose", "rvk_gp_stretch_update",
+                 "rvk_loglike", "rvk_loglike_device", "rvk_predict", "rvk_predict_device", "rvk_solve_kepler", "rvk_sync",
                  "rvk_set_option", "rvk_reserve", "rvk_post_reserve", "rvk_logpost", "rvk_logpost_device",
                  "rvk_stretch_run", "rvk_stretch_draws", "rvk_stretch_propose", "rvk_stretch_update",
                  "rvk_stretch_table_read", "rvk_copy_to_host"):

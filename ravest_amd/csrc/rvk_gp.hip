@@ -914,14 +914,16 @@ __global__ __launch_bounds__(256) void gp_logprior_kernel(PostDev pd, int n_lp, 
 // thread per proposal: q = c - (c - s) z with the draws of (step, half, j) from `pre`; the
 // log-posterior of the block of proposals is then rvk_gp_logpost_device, the accept / reject
 // stretch_accept_kernel.
+// Proposals [j0, j0 + H) of a half of hfull (the whole half on one GPU; a rank's slice when sharded).
 __global__ __launch_bounds__(256) void gp_propose_kernel(const RunArgs *__restrict__ runp, const PreDraw *__restrict__ pre,
-                                                         int D, int step, int half, long long H, double *__restrict__ q,
+                                                         int D, int step, int half, long long H, long long j0,
+                                                         long long hfull, double *__restrict__ q,
                                                          double *__restrict__ fac, double *__restrict__ lau,
                                                          long long *__restrict__ sidx) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= H) return;
     const RunArgs &run = *runp;
-    const PreDraw d = pre[((long long)step * 2 + half) * H + j];
+    const PreDraw d = pre[((long long)step * 2 + half) * hfull + j0 + j];
     const double *xs = run.x + d.s * D, *xc = run.x + d.c * D;
     for (int c = 0; c < D; ++c) q[j * D + c] = stretch_q(xc[c], xs[c], d.z);
     fac[j] = d.fac;
@@ -1406,12 +1408,66 @@ int rvk_gp_stretch_run(rvk_gp_post *p, double *d_x, double *d_lp, int64_t W, int
         for (int s = 0; s < nb; ++s)
             for (int half = 0; half < 2; ++half) {
                 hipLaunchKernelGGL(gp_propose_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, p->tab.block, D, s,
-                                   half, H, p->d_q, p->d_fac, p->d_lau, p->d_sidx);
+                                   half, H, 0LL, H, p->d_q, p->d_fac, p->d_lau, p->d_sidx);
                 if ((rc = rvk_gp_logpost_device(p, p->d_q, H, D, p->d_nlp, st))) return rc;
                 hipLaunchKernelGGL(stretch_accept_kernel, dim3(blocks), dim3(256), 0, st, p->d_run, s, H, D, p->d_q,
                                    p->d_fac, p->d_lau, p->d_sidx, p->d_nlp);
             }
     }
+    HIPCHK(hipGetLastError());
+    return RVK_OK;
+}
+
+int rvk_gp_stretch_draws(rvk_gp_post *p, int64_t W, int32_t n_steps, double a, uint64_t seed, uint64_t step0,
+                         int32_t flags, void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL GP posterior");
+    if (W < 4 || (W & 1)) return fail(RVK_E_ARG, "n_walkers must be even and >= 4");
+    if (n_steps < 1) return fail(RVK_E_ARG, "n_steps must be >= 1");
+    if (!(a > 1.0)) return fail(RVK_E_ARG, "stretch scale a must be > 1");
+    if (flags & ~RVK_STRETCH_FIXED_SPLIT) return fail(RVK_E_ARG, "unknown flags");
+    HIPCHK(hipSetDevice(p->g->h->device));
+    return draws_fill(p->tab, (hipStream_t)stream, W / 2, n_steps, p->n_free, seed, step0, a, flags);
+}
+
+int rvk_gp_stretch_propose(rvk_gp_post *p, const double *d_x, int64_t W, int32_t s, int32_t half, int64_t j0,
+                           int64_t count, double *d_out, void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL GP posterior");
+    const long long H = W / 2;
+    if (W < 4 || (W & 1) || H != p->tab.H) return fail(RVK_E_ARG, "n_walkers differs from the drawn table's");
+    if (s < 0 || s >= p->tab.steps) return fail(RVK_E_ARG, "step outside the drawn table");
+    if (half != 0 && half != 1) return fail(RVK_E_ARG, "half must be 0 or 1");
+    if (j0 < 0 || count < 0 || j0 + count > H) return fail(RVK_E_ARG, "proposal slice outside the half");
+    if (!d_x || !d_out) return fail(RVK_E_ARG, "NULL device buffer");
+    if (count == 0) return RVK_OK;
+    int rc;
+    if ((rc = gp_post_reserve_half(p, count)) || (rc = gp_post_reserve(p, count))) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(p->g->h->device));
+    const RunArgs run{const_cast<double *>(d_x), nullptr, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, nullptr, 0, 0, 2.0};
+    hipLaunchKernelGGL(set_run_kernel, dim3(1), dim3(1), 0, st, p->d_run, run);
+    hipLaunchKernelGGL(gp_propose_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, p->d_run,
+                       p->tab.block, p->n_free, s, half, (long long)count, (long long)j0, H, p->d_q, p->d_fac, p->d_lau,
+                       p->d_sidx);
+    HIPCHK(hipGetLastError());
+    return rvk_gp_logpost_device(p, p->d_q, count, p->n_free, d_out, st);
+}
+
+int rvk_gp_stretch_update(rvk_gp_post *p, double *d_x, double *d_lp, int64_t W, int32_t s, int32_t half,
+                          const double *d_nlp, double *d_chain_step, double *d_lnp_step, const int64_t *d_nacc_in,
+                          int64_t *d_nacc_out, int32_t *d_status, void *stream) {
+    if (!p) return fail(RVK_E_ARG, "NULL GP posterior");
+    const long long H = W / 2;
+    if (W < 4 || (W & 1) || H != p->tab.H) return fail(RVK_E_ARG, "n_walkers differs from the drawn table's");
+    if (s < 0 || s >= p->tab.steps) return fail(RVK_E_ARG, "step outside the drawn table");
+    if (half != 0 && half != 1) return fail(RVK_E_ARG, "half must be 0 or 1");
+    if (!d_x || !d_lp || !d_nlp || !d_status) return fail(RVK_E_ARG, "NULL device buffer");
+    if (d_nacc_out && !d_nacc_in) return fail(RVK_E_ARG, "d_nacc_out needs d_nacc_in");
+    HIPCHK(hipSetDevice(p->g->h->device));
+    hipLaunchKernelGGL(stretch_update_kernel, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       p->tab.block + ((size_t)s * 2 + (size_t)half) * (size_t)H, H, p->n_free, d_x, d_lp, d_nlp,
+                       (const long long *)d_nacc_in, (long long *)d_nacc_out, (int *)d_status, d_chain_step,
+                       d_lnp_step);
     HIPCHK(hipGetLastError());
     return RVK_OK;
 }

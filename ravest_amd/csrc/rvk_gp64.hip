@@ -138,10 +138,58 @@ __device__ __forceinline__ void load_frags(P tile, double (&f)[2][8], int lane) 
 struct QP {
     double amp2, gam, inv_per, inv_le;
 };
+#ifndef RVK_GP64_FASTCOV
+#define RVK_GP64_FASTCOV 1   // lean sin(pi u) and exp (below); 0: the device library's sinpi / exp
+#endif
+// sin(pi u)^2 for any finite u: u - rint(u) is exact and |r| <= 1/2, sin(pi u) = +-sin(pi r);
+// sin(pi r) = pi r + r^3 Q(r^2) (least-squares fit, <= 2.7 ulp measured on [0, 1/2]) with pi
+// split hi + lo so the leading term rounds once.  NaN / inf propagate as NaN.
+__device__ __forceinline__ double sinpi_sq(double u) {
+    const double r = u - __builtin_rint(u);
+    const double r2 = r * r;
+    double q = fma_s(r2, 7.696389727699914e-07, -2.1903364526655565e-05);
+    q = fma_s(r2, q, 0.0004662997683854282);
+    q = fma_s(r2, q, -0.007370430497584462);
+    q = fma_s(r2, q, 0.0821458865724345);
+    q = fma_s(r2, q, -0.5992645293189337);
+    q = fma_s(r2, q, 2.550164039877302);
+    q = fma_s(r2, q, -5.167712780049969);
+    const double s = __builtin_fma(r, 3.141592653589793, r * fma_s(r2, q, 1.2246467991473532e-16));
+    return s * s;
+}
+// exp(x) for x <= 0 (the covariance's exponent): k = rint(x / ln 2), r = x - k ln 2 in two parts
+// (|r| <= ln2 / 2), exp(r) = 1 + r (1 + r P(r)) (least-squares fit, <= 1.3 ulp measured), 2^k by
+// ldexp (0 below the subnormal range).  ocml's exp adds range and special-value checks the
+// covariance never needs.
+__device__ __forceinline__ double exp_nonpos(double x) {
+    x = x < -800.0 ? -800.0 : x;                        // -inf -> 0 like exp (NaN passes: compare false)
+    const double k = __builtin_rint(x * 1.4426950408889634);
+    double r = __builtin_fma(k, -0.6931471805599453, x);
+    r = __builtin_fma(k, -2.3190468138462996e-17, r);
+    double p = fma_s(r, 2.50246452096493e-08, 2.7631125446226205e-07);
+    p = fma_s(r, p, 2.755750728541229e-06);
+    p = fma_s(r, p, 2.480149034623507e-05);
+    p = fma_s(r, p, 0.00019841269597118904);
+    p = fma_s(r, p, 0.0013888888946678828);
+    p = fma_s(r, p, 0.008333333333451433);
+    p = fma_s(r, p, 0.04166666666651632);
+    p = fma_s(r, p, 0.16666666666666483);
+    p = fma_s(r, p, 0.5000000000000012);
+    p = __builtin_fma(r, __builtin_fma(r, p, 1.0), 1.0);
+    int ki;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));   // saturating (k <= 0 here)
+    return __builtin_ldexp(p, ki);
+}
 __device__ __forceinline__ double qp_cov(const QP &h, double tau) {
+#if RVK_GP64_FASTCOV
+    const double sn2 = sinpi_sq(fabs(tau) * h.inv_per);
+    const double x = tau * h.inv_le;
+    return h.amp2 * exp_nonpos(-(h.gam * sn2 + 0.5 * (x * x)));
+#else
     const double sn = sinpi(fabs(tau) * h.inv_per);
     const double x = tau * h.inv_le;
     return h.amp2 * exp(-(h.gam * (sn * sn) + 0.5 * (x * x)));
+#endif
 }
 
 // The diagonal factor of one step, one wave (its own register allocation: a 32-double row or

@@ -137,11 +137,13 @@ class ShardedDevicePosterior:
 
 class LibStretchOps:
     """The device stretch move's operations for ShardedDeviceSampler, on librvk
-    (include/rvk_post.h): draws, slice evaluation, whole-half update."""
+    (include/rvk_post.h): draws, slice evaluation, whole-half update.  ``gp=True``: the GP
+    log-posterior's (include/rvk_gp.h rvk_gp_stretch_*), GPFitter.run_mcmc's sampler."""
 
-    def __init__(self, post) -> None:
+    def __init__(self, post, gp: bool = False) -> None:
         self.post = post
         self.n_free = post.n_free
+        self._pre = "rvk_gp_stretch_" if gp else "rvk_stretch_"
 
     def reserve(self, n: int) -> None:
         self.post.reserve(n)
@@ -151,18 +153,21 @@ class LibStretchOps:
 
     def draws(self, W, n, a, seed, step0, flags, stream) -> None:
         from . import _lib
-        _lib.check(_lib.load().rvk_stretch_draws(self.post._p, W, n, a, seed, step0, flags, stream.cuda_stream))
+        _lib.check(getattr(_lib.load(), self._pre + "draws")(self.post._p, W, n, a, seed, step0, flags,
+                                                               stream.cuda_stream))
 
     def propose(self, x, W, s, half, j0, count, out, stream) -> None:
         from . import _lib
-        _lib.check(_lib.load().rvk_stretch_propose(self.post._p, x.data_ptr(), W, s, half, j0, count, out.data_ptr(),
-                                                   stream.cuda_stream))
+        _lib.check(getattr(_lib.load(), self._pre + "propose")(self.post._p, x.data_ptr(), W, s, half, j0, count,
+                                                                 out.data_ptr(), stream.cuda_stream))
 
     def update(self, x, lp, W, s, half, nlp, chain_step, lnp_step, nacc_in, nacc_out, status, stream) -> None:
         from . import _lib
-        _lib.check(_lib.load().rvk_stretch_update(self.post._p, x.data_ptr(), lp.data_ptr(), W, s, half, nlp.data_ptr(),
-                                                  chain_step.data_ptr(), lnp_step.data_ptr(), nacc_in.data_ptr(),
-                                                  nacc_out.data_ptr(), status.data_ptr(), stream.cuda_stream))
+        _lib.check(getattr(_lib.load(), self._pre + "update")(self.post._p, x.data_ptr(), lp.data_ptr(), W, s, half,
+                                                                nlp.data_ptr(), chain_step.data_ptr(),
+                                                                lnp_step.data_ptr(), nacc_in.data_ptr(),
+                                                                nacc_out.data_ptr(), status.data_ptr(),
+                                                                stream.cuda_stream))
 
 
 from .sampler import _Chunk, _DevicePipeline  # noqa: E402
@@ -188,7 +193,9 @@ class ShardedDeviceSampler(_DevicePipeline):
     ``keep_chain``: "all", or the rank that stores the chain (in its HBM with the default
     ``chain_storage``, or its host memory with "host"; the others keep only the device chunk);
     ``get_autocorr_time`` is computed on that rank (rank 0 for "all") and broadcast, so call it
-    on every rank, as ravest's convergence loop does."""
+    on every rank, as ravest's convergence loop does.  A ``GPLogPosterior`` (GPFitter.run_mcmc,
+    fit.py:4983-4990) shards the same way over rvk_gp_stretch_draws / _propose / _update; its
+    chain equals DeviceEnsembleSampler(GPLogPosterior)'s bit for bit."""
 
     def __init__(self, log_posterior, nwalkers: int, a: float = 2.0, seed: int = 0, group=None,
                  randomize_split: bool = True, steps_per_call: int = 256, keep_chain="all",
@@ -198,12 +205,12 @@ class ShardedDeviceSampler(_DevicePipeline):
         if ops is None:
             from .gp import DeviceGPPosterior, GPLogPosterior
             from .posterior import DevicePosterior
-            if isinstance(log_posterior, (GPLogPosterior, DeviceGPPosterior)):
-                raise TypeError("ShardedDeviceSampler shards the Keplerian log-posterior (rvk_stretch_propose / "
-                                "rvk_stretch_update); a GP posterior runs on one GPU per chain with "
-                                "DeviceEnsembleSampler")
-            post = log_posterior if isinstance(log_posterior, DevicePosterior) else DevicePosterior(log_posterior)
-            ops = LibStretchOps(post)
+            if isinstance(log_posterior, (GPLogPosterior, DeviceGPPosterior)):      # GPFitter.run_mcmc
+                post = log_posterior if isinstance(log_posterior, DeviceGPPosterior) else DeviceGPPosterior(log_posterior)
+                ops = LibStretchOps(post, gp=True)
+            else:
+                post = log_posterior if isinstance(log_posterior, DevicePosterior) else DevicePosterior(log_posterior)
+                ops = LibStretchOps(post)
             device = torch.device("cuda", torch.cuda.current_device())
         self.ops = ops
         self.nwalkers, self.ndim, self.a, self.seed = nwalkers, ops.n_free, float(a), int(seed)

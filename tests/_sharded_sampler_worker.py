@@ -15,6 +15,14 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def gp_posterior(W):
+    """A GP log-posterior of the reference's golden case a and W finite starting walkers."""
+    from tests.test_gpu_gp64 import _gpost, _load_gp_case
+    c = _load_gp_case("a")
+    gp = _gpost(c, "fp64")
+    return gp, np.ascontiguousarray(c["x"][np.isfinite(c["log_prob"])][:W])
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -29,13 +37,17 @@ def main():
         dist.init_process_group(backend)
     world, rank = dist.get_world_size(), dist.get_rank()
     W, steps = int(sys.argv[2]), int(sys.argv[3])
-    lpost, x0 = make_posterior(2, W, seed=4, device=local)
+    gp = len(sys.argv) > 4 and sys.argv[4] == "gp"
+    if gp:                                           # GPFitter.run_mcmc's posterior (reference goldens, case a)
+        lpost, x0 = gp_posterior(W)
+    else:
+        lpost, x0 = make_posterior(2, W, seed=4, device=local)
     s = ShardedDeviceSampler(lpost, W, seed=77, steps_per_call=4, keep_chain=0)
     assert s.grouped
     s.run_mcmc(x0, steps)
     tau = s.get_autocorr_time(tol=0)                 # computed on rank 0, broadcast to every rank
     res = {}
-    if backend == "nccl":                            # device-resident posterior sharding (config 4's form)
+    if backend == "nccl" and not gp:                 # device-resident posterior sharding (config 4's form)
         from ravest_amd.engine import RVEngine
         ds = make_config(2, n_walkers=4096 + 3)
         eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, ds.parameterisation, ds.t0, device=local)

@@ -43,33 +43,42 @@ def test_sharded_sampler_one_rank_equals_single_gpu(randomize):
     assert sh.exchange_bytes_per_half_step == (W // 2) * 8
 
 
-def test_sharded_sampler_rejects_gp_posterior():
+def _single_gp(W, steps):
+    from ravest_amd.sampler import DeviceEnsembleSampler
+    from tests._sharded_sampler_worker import gp_posterior
+    gp, x0 = gp_posterior(W)
+    s = DeviceEnsembleSampler(gp, W, seed=77, steps_per_call=5)
+    s.run_mcmc(x0, steps)
+    return s
+
+
+def test_sharded_gp_sampler_one_rank_equals_single_gpu():
+    """GPFitter.run_mcmc's sampler sharded (rvk_gp_stretch_draws / _propose / _update) equals the
+    single-GPU rvk_gp_stretch_run chain bit for bit (no process group: one rank)."""
     from ravest_amd.distributed import ShardedDeviceSampler
-    from ravest_amd.gp import GPKernel, GPLogPosterior
-    from ravest_amd.synth import make_dataset
-    from ravest_amd import prior as P
-    ds = make_dataset(1, 40, 1, seed=3)
-    free = ["P_b", "K_b"]
-    fixed = {n: float(ds.truth[n]) for n in ds.names if n not in free}
-    gp = GPLogPosterior(ds.planet_letters, ds.parameterisation, GPKernel("Quasiperiodic"),
-                        {"P_b": P.Uniform(1, 100), "K_b": P.Uniform(0, 100)}, {},
-                        fixed, {"gp_amp": 2.0, "gp_lambda_e": 50.0, "gp_lambda_p": 0.5, "gp_period": 20.0}, free, [],
-                        ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments)
-    with pytest.raises(TypeError, match="GP posterior"):
-        ShardedDeviceSampler(gp, 16)
+    from tests._sharded_sampler_worker import gp_posterior
+    W, steps = 32, 8
+    gp, x0 = gp_posterior(W)
+    sh = ShardedDeviceSampler(gp, W, seed=77, steps_per_call=3)
+    sh.run_mcmc(x0, steps)
+    ref = _single_gp(W, steps)
+    assert np.array_equal(sh.get_chain(), ref.get_chain())
+    assert np.array_equal(sh.get_log_prob(), ref.get_log_prob())
+    assert np.array_equal(sh.naccepted, ref.naccepted) and ref.naccepted.sum() > 0
+    assert sh.exchange_bytes_per_half_step == (W // 2) * 8
 
 
-def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2):
-    out = tmp_path / f"chain_{backend}_{nproc}.npz"
+def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2, gp=False):
+    out = tmp_path / f"chain_{backend}_{nproc}{'_gp' if gp else ''}.npz"
     env = dict(os.environ, RVK_TEST_BACKEND=backend, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "_sharded_sampler_worker.py"),
-           str(out), str(W), str(steps)]
+           str(out), str(W), str(steps)] + (["gp"] if gp else [])
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     got = np.load(out)
     assert int(got["world"]) == nproc
-    ref = _single(W, steps)
+    ref = _single_gp(W, steps) if gp else _single(W, steps)
     assert np.array_equal(got["chain"], ref.get_chain())
     assert np.array_equal(got["lnp"], ref.get_log_prob())
     assert np.array_equal(got["nacc"], ref.naccepted)
@@ -84,6 +93,16 @@ def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2):
 
 def test_sharded_sampler_two_ranks_gloo(tmp_path):
     _run_ranks(tmp_path, "gloo", 29533)
+
+
+def test_sharded_gp_sampler_two_ranks_gloo(tmp_path):
+    """GPFitter.run_mcmc's sampler over two ranks (gloo, both on cuda:0): each rank evaluates half of
+    every half-step's GP proposals; the chain equals the single-GPU GP sampler's bit for bit."""
+    _run_ranks(tmp_path, "gloo", 29536, W=32, steps=6, gp=True)
+
+
+def test_rccl_world_one_gp(tmp_path):
+    _run_ranks(tmp_path, "nccl", 29537, W=32, steps=6, nproc=1, gp=True)
 
 
 def test_rccl_world_one(tmp_path):
