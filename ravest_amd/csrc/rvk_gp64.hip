@@ -286,14 +286,55 @@ struct Ops64 {
     double2 b[R][2];
 };
 
+// The tile rows a row-owning wave owns, ascending (so the rows still live at a step are a suffix).
+// Default: wr, wr + NA, wr + 2 NA, ...  RVK_GP64_BAL (nt == 16, 7 row waves, MAXR 3): a table that
+// evens out each SIMD's matrix-pipe work per step (waves w and w + 4 share SIMD w mod 4; wave 7
+// factors): summed over the 16 steps, the busiest SIMD's accumulation + S1 + S2 MFMAs drop from
+// 9312 to 8192 (of 6400 per SIMD if perfectly even).
+#ifndef RVK_GP64_BAL
+#define RVK_GP64_BAL 0
+#endif
+template <int MAXR>
+struct RowMap {
+    int bi[MAXR];
+    int nown;
+};
+template <int MAXR, int NA>
+__device__ __forceinline__ RowMap<MAXR> row_map(int wr, int nt) {
+    RowMap<MAXR> m;
+    m.nown = 0;
+#pragma unroll
+    for (int q = 0; q < MAXR; ++q) m.bi[q] = wr + NA * q;
+    m.nown = wr < nt ? (nt - wr + NA - 1) / NA : 0;
+    if constexpr (RVK_GP64_BAL && RVK_GP64_RING > 1 && MAXR == 3 && NA == 7) {
+        if (nt == 16) {
+            constexpr int tab[7][3] = {{2, 10, 99}, {3, 11, 99}, {0, 1, 8}, {5, 9, 12}, {4, 13, 99}, {7, 14, 99}, {6, 15, 99}};
+            constexpr int cnt[7] = {2, 2, 3, 3, 2, 2, 2};
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                int v = 99;
+#pragma unroll
+                for (int w = 0; w < 7; ++w) v = wr == w ? tab[w][q] : v;
+                m.bi[q] = v;
+            }
+            int c = 0;
+#pragma unroll
+            for (int w = 0; w < 7; ++w) c = wr == w ? cnt[w] : c;
+            m.nown = c;
+        }
+    }
+    return m;
+}
+
 template <int MAXR, int NA, int A, int B, int D>
-__device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, int wr, int lane) {
+__device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, const RowMap<MAXR> &rm,
+                                           int lane) {
     constexpr int R = B - A + 1;
     const int NQ = 4 * k;                           // quarters (j, part), j < k
     const double2 *rowa = reinterpret_cast<const double2 *>(wk + tix(k + 1, 0) * TILE) + lane;
     const double2 *rowb[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) rowb[r] = reinterpret_cast<const double2 *>(wk + tix(wr + NA * (A + r), 0) * TILE) + lane;
+    for (int r = 0; r < R; ++r) rowb[r] = reinterpret_cast<const double2 *>(wk + tix(rm.bi[A + r], 0) * TILE) + lane;
     Ops64<R> ops[D];
     auto issue = [&](Ops64<R> &o, int hx) {         // unconditional (clamped past the end): the
         hx = hx < NQ ? hx : NQ - 1;                 // wait counts stay exact on every path
@@ -334,13 +375,13 @@ __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__res
 
 // The live rows A0 .. B0 of a wave (a suffix of its rows: rows finish in order), in spans of <= 3.
 template <int MAXR, int NA, int D>
-__device__ __forceinline__ void accum_rows(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, int wr, int lane,
-                                           int a0, int b0) {
+__device__ __forceinline__ void accum_rows(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, const RowMap<MAXR> &rm,
+                                           int lane, int a0, int b0) {
     for (int a = a0; a <= b0; a += 3) {
         const int b = a + 2 < b0 ? a + 2 : b0;
 #define RVK_SPAN(X, Y)                                                                   \
     if constexpr (Y < MAXR) {                                                            \
-        if (a == X && b == Y) accum_span<MAXR, NA, X, Y, D>(acc, wk, k, wr, lane);       \
+        if (a == X && b == Y) accum_span<MAXR, NA, X, Y, D>(acc, wk, k, rm, lane);       \
     }
         RVK_SPAN(0, 0) RVK_SPAN(0, 1) RVK_SPAN(0, 2) RVK_SPAN(1, 1) RVK_SPAN(1, 2) RVK_SPAN(1, 3)
         RVK_SPAN(2, 2) RVK_SPAN(2, 3) RVK_SPAN(2, 4) RVK_SPAN(3, 3) RVK_SPAN(3, 4) RVK_SPAN(4, 4)
@@ -468,13 +509,21 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     for (int i = 0; i < 4; ++i)
                         fb[(16 * q + (lane & 15)) * FS + 16 * p + (lane >> 4) + 4 * i] = -A.c[p][q][i];
         };
+        const RowMap<MAXR> rm = row_map<MAXR, NA>(wr, nt);   // the non-grouped shapes' row ownership
+        auto col0 = [&](int bi) {
+            Acc t;
+            cov_tile(bi, 0, t);
+            if (bi == 0) put_diag(t);
+            else if constexpr (LDSP) park(pslot(bi), t, lane);
+            else park(wk + tix(bi, 0) * TILE, t, lane);
+        };
         if (wr < NA) {
-            for (int bi = wr; bi < nt; bi += NA) {          // every owned row (also past MAXR: grouped)
-                Acc t;
-                cov_tile(bi, 0, t);
-                if (bi == 0) put_diag(t);
-                else if constexpr (LDSP) park(pslot(bi), t, lane);
-                else park(wk + tix(bi, 0) * TILE, t, lane);
+            if constexpr (GROUPED) {
+                for (int bi = wr; bi < nt; bi += NA) col0(bi);   // every owned row (also past MAXR)
+            } else {
+#pragma unroll
+                for (int q = 0; q < MAXR; ++q)
+                    if (q < rm.nown) col0(rm.bi[q]);
             }
         }
         __syncthreads();
@@ -505,7 +554,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
         } else {
             // ---- the row owners: the next column's accumulation, S1, S2 --------------------------
             Acc nacc[MAXR];
-            const int nown = (nt - wr + NA - 1) / NA;       // rows bi = wr + NA q < nt this wave owns
+            const int nown = GROUPED ? (nt - wr + NA - 1) / NA : rm.nown;   // rows this wave owns
             constexpr bool grouped = GROUPED;               // more rows than accumulator registers
             for (int k = 0; k < nt; ++k) {
                 G64_MARK(k, 0);
@@ -514,8 +563,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     if (grouped && wr + NA * (qo + MAXR - 1) < k + 1) continue;    // the group's rows are finished
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
-                        const int bi = wr + NA * (qo + q);
-                        if (bi >= k + 1 && bi < nt) cov_tile(bi, k + 1, nacc[q]);
+                        const int bi = grouped ? wr + NA * (qo + q) : rm.bi[q];
+                        if (bi >= k + 1 && bi < nt && (grouped || q < nown)) cov_tile(bi, k + 1, nacc[q]);
                     }
                     // operands: the A tile L(k+1, j) and the B tiles L(bi, j) of two owned rows at a time,
                     // a quarter tile (2 of the 8 k-steps) per register set; sets X / Y alternate so the
@@ -583,9 +632,12 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     };
                     if constexpr (!grouped && RVK_GP64_RING > 1) {
                         // the live rows (a suffix of the owned ones), software-pipelined
-                        const int r0 = k + 1 > wr ? (k + 1 - wr + NA - 1) / NA : 0;
+                        int r0 = nown;                          // the first live row
+#pragma unroll
+                        for (int q = MAXR - 1; q >= 0; --q)
+                            if (q < nown && rm.bi[q] >= k + 1) r0 = q;
                         if (k > 0 && r0 < nown && !(RVK_GP64_ABLATE & 8))
-                            accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, wr, lane, r0, nown - 1);
+                            accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, rm, lane, r0, nown - 1);
                     } else {
                         pass(std::integral_constant<int, 0>{});
                         if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
@@ -625,8 +677,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     for (int i = 0; i < 4; ++i) yv[p][i] = Lr[k * TB + 16 * p + (lane >> 4) + 4 * i];
 #pragma unroll
                 for (int q = 0; q < (grouped ? nown : MAXR); ++q) {
-                    const int bi = wr + NA * q;
-                    if (bi > k && bi < nt) {
+                    const int bi = grouped ? wr + NA * q : rm.bi[q];
+                    if (bi > k && bi < nt && q < nown) {
                         double *T = wk + tix(bi, k) * TILE;
                         Acc cur;
                         if constexpr (LDSP) unpark(pslot(bi), cur, lane);
@@ -693,8 +745,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 if constexpr (!grouped) {
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
-                        const int bi = wr + NA * q;
-                        if (bi > k && bi < nt) s2(nacc[q], bi);
+                        const int bi = rm.bi[q];
+                        if (bi > k && bi < nt && q < nown) s2(nacc[q], bi);
                     }
                 } else {
                     for (int q = 0; q < nown; ++q) {
