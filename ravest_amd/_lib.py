@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "librvk.so")
+_DEFAULT_PATH = LIB_PATH = os.path.join(_HERE, "lib", "librvk.so")
 # experiment hook: A/B builds of the same source (tools/variants.sh); never set in production
 LIB_PATH = os.environ.get("RAVEST_AMD_LIB", LIB_PATH)
 
@@ -61,6 +61,25 @@ def prior_src_default(planet: int, j: int) -> int:
 _lib = None
 
 
+class _Tolerant:
+    """Experiment hook only (RAVEST_AMD_LIB): wraps an older library so binding a symbol it lacks
+    is a no-op; calling one raises AttributeError as usual."""
+
+    class _Missing:
+        argtypes = restype = None
+
+    def __init__(self, lib) -> None:
+        self.__dict__["_lib"] = lib
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._lib, name)
+        except AttributeError:
+            if name.startswith("rvk_"):
+                return _Tolerant._Missing()
+            raise
+
+
 class RVKError(RuntimeError):
     pass
 
@@ -79,6 +98,8 @@ def load() -> C.CDLL:
         raise RVKError(f"{LIB_PATH} not found: the HIP extension is not built "
                        "(run __graft_entry__.build() or `make -C ravest_amd`)")
     L = C.CDLL(LIB_PATH)
+    if LIB_PATH != _DEFAULT_PATH:
+        L = _Tolerant(L)     # A/B against an older build: symbols it lacks are skipped, not bound
     dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int32), C.c_void_p
     L.rvk_create.argtypes = [dp, dp, dp, ip, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_int32]
     L.rvk_create.restype = vp

@@ -141,7 +141,10 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     // SAMPLE & 4 (ALLP): every prior kind in the fused prep (else the basic kinds only);
     // SAMPLE & 8 (CONV): + the prior-side conversion (Case 3; an out-of-line call, whose frame
     // only this variant pays).
+    // SAMPLE & 16 (DIRECT, with MODE 3): the walker's free coordinates are given (sa.q, row stride
+    // sa.qstride) instead of proposed -- the device log-posterior in one kernel (rvk_logpost[_device]).
     constexpr int MODE = SAMPLE & 3;
+    constexpr bool DIRECT = (SAMPLE & 16) != 0;
     constexpr bool FUSE = MODE >= 2;
     constexpr bool ACCEPT = MODE == 1 || MODE == 2;
     constexpr bool CONV = (SAMPLE & 8) != 0;
@@ -182,8 +185,16 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     };
     auto fetch = [&](long long w) {
         Fetch f;
-        const RunArgs &run = *sa.run;
         const int D = sa.pd.n_free;
+        if constexpr (DIRECT) {
+            f.s = w;
+            f.c = 0;
+            f.z = f.fac = f.lau = f.lpo = f.b = 0.0;
+            f.nacc = 0;
+            f.a = lane < D ? sa.q[w * sa.qstride + lane] : 0.0;
+            return f;
+        }
+        const RunArgs &run = *sa.run;
         const long long j = sa.j0 + w;   // global proposal index within the half
         const PreDraw p = sa.pre[((long long)sa.step * 2 + sa.half) * sa.hfull + j];
         f.s = p.s;
@@ -248,8 +259,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 const int D = pd.n_free;
                 const Fetch f = (base == (long long)blockIdx.x * wb && j == wv) ? pre : fetch(w);
                 lp_old_s = f.lpo;                         // (needed only in the epilogue)
-                const double q_s = lane < D ? stretch_q(f.b, f.a, f.z) : 0.0;
-                if (lane < D) {                           // parked for the epilogue (read back by the same lane)
+                const double q_s = lane < D ? (DIRECT ? f.a : stretch_q(f.b, f.a, f.z)) : 0.0;
+                if (ACCEPT && lane < D) {                 // parked for the epilogue (read back by the same lane)
                     fq[j][lane] = q_s;
                     fx[j][lane] = f.a;
                 }
@@ -1066,6 +1077,9 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->sample_eval[1] = pick_sample<7>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_fused[2] = pick_sample<14>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_eval[2] = pick_sample<15>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_direct[0] = pick_sample<19>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_direct[1] = pick_sample<23>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_direct[2] = pick_sample<31>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;

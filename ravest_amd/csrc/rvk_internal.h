@@ -145,6 +145,8 @@ struct rvk_handle {
     // (rvk_stretch_propose); [1]: every prior kind, [2]: + the prior-side conversion in the prep
     rvk::sample_launch_t sample_fused[3] = {nullptr, nullptr, nullptr};
     rvk::sample_launch_t sample_eval[3] = {nullptr, nullptr, nullptr};
+    // ... and the given free coordinates' log-posteriors (rvk_logpost_device in one kernel)
+    rvk::sample_launch_t sample_direct[3] = {nullptr, nullptr, nullptr};
     int solver = 0;
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW

@@ -99,6 +99,7 @@ struct rvk_post {
     int n_free = 0, n_prior = 0;
     bool convert = false;
     bool fusable = false;                  // proposals can be made inside the likelihood kernel
+    bool two_kernel = false;               // rvk_logpost_device: logprior_kernel + likelihood (RVK_LOGPOST_FUSE=0)
     int ext = 0;                           // ... 1: with a transcendental prior kind, 2: + the conversion
     double jac = 0.0, renorm = 0.0;
     int32_t *d_colmap = nullptr;
@@ -266,6 +267,8 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
     // hook) keeps the two-kernel path.
     const char *fe = getenv("RVK_SAMPLER_FUSE");
     p->fusable = n_free <= kFuseMaxD && pf <= kFuseMaxPFull && n_prior <= kFuseMaxPrior && !(fe && atoi(fe) == 0);
+    const char *le = getenv("RVK_LOGPOST_FUSE");        // experiment / test hook: the two-kernel form
+    p->two_kernel = le && atoi(le) == 0;
     bool basic = true;
     for (int k = 0; k < n_prior; ++k) basic &= kind[k] <= kMaxBasicPriorKind;
     p->ext = convert ? 2 : basic ? 0 : 1;
@@ -374,6 +377,20 @@ int rvk_logpost_device(rvk_post *p, const double *d_free, int64_t W, int64_t str
     hipStream_t st = (hipStream_t)stream;
     rvk_handle *h = p->h;
     HIPCHK(hipSetDevice(h->device));
+    if (p->fusable && h->solver == 0 && h->sample_direct[p->ext] && !p->two_kernel) {
+        // one kernel: each wave builds its walker's row, jitter check, conversion and priors
+        // lane-parallel (the fused sampler's prep on the given coordinates), then the epoch loop
+        SampleArgs sa{};
+        sa.D = p->n_free;
+        sa.q = d_free;
+        sa.qstride = stride;
+        sa.pd = p->dev();
+        sa.out = d_out;
+        h->sample_direct[p->ext](st, h->epochs(), h->n, h->n_inst, nullptr, W, h->p_full(),
+                                 PostArgs{nullptr, p->jac, p->renorm}, sa);
+        HIPCHK(hipGetLastError());
+        return RVK_OK;
+    }
     hipLaunchKernelGGL(logprior_kernel, dim3(wave_blocks(W)), dim3(256), 0, st, p->dev(), d_free, (long long)W,
                        (long long)stride, p->d_full, p->d_lp);
     h->launch(st, h->epochs(), h->n, h->n_inst, p->d_full, W, h->p_full(), d_out, PostArgs{p->d_lp, p->jac, p->renorm});

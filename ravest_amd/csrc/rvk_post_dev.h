@@ -415,6 +415,7 @@ struct SampleArgs {
     long long hfull;            // walkers per half (the complement's range; chain row stride / 2)
     const PreDraw *pre;         // [steps][2][hfull] the draws, indexed by (step, half, j0 + w)
     double *out;                // SAMPLE == 3: out[w] = the proposal's log-posterior (no accept / reject)
+    long long qstride;          // SAMPLE & 16 (DIRECT): row stride of q, the given free coordinates
 };
 
 // Limits of the fused proposal path (loglike_kernel SAMPLE >= 2): lane c of the walker's wave

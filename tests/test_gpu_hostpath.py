@@ -140,3 +140,17 @@ def test_engine_loglike_every_transport_large():
         assert np.array_equal(res[mode][0], res["pageable"][0])
         assert np.array_equal(res[mode][1], res["pageable"][1])
     assert np.array_equal(res["auto"][1], res["auto"][0][:3])
+
+
+@pytest.mark.parametrize("name", logpost_cases())
+def test_one_kernel_logpost_equals_two_kernel_path(name, monkeypatch):
+    """rvk_logpost_device runs as ONE kernel (the fused sampler's lane-parallel prep on the given
+    coordinates) when the posterior fits the fused limits; RVK_LOGPOST_FUSE=0 keeps the two-kernel
+    form (logprior_kernel + the likelihood's posterior epilogue).  Same bits, every golden."""
+    case = load_case(name)
+    x = case["theta_free"]
+    one = _posterior(case).device_posterior()(x)
+    monkeypatch.setenv("RVK_LOGPOST_FUSE", "0")
+    two = _posterior(case).device_posterior()(x)
+    assert np.array_equal(one, two, equal_nan=True)
+    assert_ll_close(one, case["log_prob"], what=f"one-kernel-{name}")

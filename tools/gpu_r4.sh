@@ -8,8 +8,13 @@ O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 SEL=${@:-tests}
-timeout -k 10 900 python -u -m pytest $SEL -m gpu -x -v --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error|error" $O/pytest_gpu.log | head -30; tail -40 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest $SEL -m gpu --maxfail=8 -v --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?
 tail -3 $O/pytest_gpu.log
+if [ $rc -ne 0 ]; then
+  echo "pytest rc=$rc"; grep -E "^FAILED|^ERROR|Error:" $O/pytest_gpu.log | head -30
+  [ $rc -eq 1 ] || exit 1          # only ordinary test failures go on to the measurements
+fi
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 timeout -k 10 180 python tools/host_step_probe.py > $O/host_probe.json 2> $O/host_probe.err || { tail -20 $O/host_probe.err; exit 1; }
 cat $O/host_probe.json
