@@ -71,6 +71,9 @@ namespace {
 #ifndef RVK_GP_RPASS
 #define RVK_GP_RPASS 2    // rows per accumulation pass (the A tiles are re-read once per pass)
 #endif
+#ifndef RVK_GP_SCHEDB
+#define RVK_GP_SCHEDB 0   // scheduling barriers around each ring set's loads and MFMAs (fp64: see rvk_gp64.hip)
+#endif
 #ifndef RVK_GP_NBUF
 #define RVK_GP_NBUF 2     // operand register sets in the ring (NBUF - 1 in flight)
 #endif
@@ -663,7 +666,9 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
 #pragma unroll
                         for (int b = 0; b < NB; ++b) {
                             issue(ring[(b + NB - 1) % NB], hx + b + NB - 1);
+                            if (RVK_GP_SCHEDB) __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead
                             if (b == 0 || hx + b < H1) consume(ring[b], hx + b);
+                            if (RVK_GP_SCHEDB) __builtin_amdgcn_sched_barrier(0);
                         }
                     }
                 };

@@ -4,6 +4,7 @@
 TAG=${1:-r4b}
 bash tools/gpu_r4.sh $TAG || exit 1
 bash tools/gp64_ab.sh ${TAG}_gp || exit 1
+SKIPTEST=1 VARDIR=varlib/f32 bash tools/gp64_ab.sh ${TAG}_gp32 fp32+fp64 || exit 1
 O=gpurun_out/${TAG}_kb
 mkdir -p $O
 for rep in 1 2 3; do

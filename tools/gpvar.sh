@@ -6,17 +6,18 @@ set -e
 cd "$(dirname "$0")/.."
 TU=rvk_gp64.hip
 if [ "$1" = "-u" ]; then TU=$2; shift 2; fi
-mkdir -p varlib build/varobj
+OUT=${VAROUT:-varlib}
+mkdir -p $OUT build/varobj
 OTHERS=$(ls build/obj/*.o | grep -v "/${TU%.hip}.o$")
 one() {
   name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c \
     -o build/varobj/${TU%.hip}_$name.o ravest_amd/csrc/$TU -Rpass-analysis=kernel-resource-usage 2> build/varobj/$name.res
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o varlib/librvk_$name.so build/varobj/${TU%.hip}_$name.o $OTHERS
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/librvk_$name.so build/varobj/${TU%.hip}_$name.o $OTHERS
 }
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   one $name $flags &
 done
 wait
-ls -la varlib
+ls -la $OUT
