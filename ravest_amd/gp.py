@@ -314,9 +314,12 @@ class GPLogPosterior:
     __call__ = log_probability_batch
 
     def log_probability(self, combined_params_hyperparams: Dict[str, float]) -> float:
-        row = np.array([[combined_params_hyperparams[n]
-                         for n in self.free_params_names + self.free_hyperparams_names]], dtype=np.float64)
-        return float(self.log_probability_batch(row)[0])
+        """fit.py:7836-7901 for one walker ({name: value}); a dict of arrays (emcee with
+        parameter_names and vectorize=True) gives every walker's value in one device call."""
+        vals = [combined_params_hyperparams[n] for n in self.free_params_names + self.free_hyperparams_names]
+        if np.ndim(vals[0]) > 0:
+            return self.log_probability_batch(np.stack([np.asarray(v, np.float64) for v in vals], axis=1))
+        return float(self.log_probability_batch(np.array([vals], dtype=np.float64))[0])
 
     def _negative_log_probability_for_MAP(self, combined_free_params_hyperparams_vals) -> float:
         """fit.py:7903-7939."""

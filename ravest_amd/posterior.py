@@ -13,7 +13,7 @@ Entry points:
   * ``log_probability_batch(theta_free[W, D]) -> ndarray[W]`` -- the
     vectorised drop-in (emcee ``vectorize=True``); ``__call__`` is the same.
 Both route through the device log-posterior (``DevicePosterior``: the scatter,
-jitter check, conversion, priors, likelihood and corrections in two kernels,
+jitter check, conversion, priors, likelihood and corrections in one kernel,
 one host round trip) whenever every prior is one of ravest's built-in classes;
 a custom callable prior keeps the host-side prior path (``route="host"``).
 Mask semantics follow fit.py:3461-3495 exactly: jitter < 0, a prior-side
@@ -269,7 +269,14 @@ class LogPosterior:
     __call__ = log_probability_batch
 
     def log_probability(self, free_params_dict: Dict[str, float]) -> float:
-        row = np.array([[free_params_dict[n] for n in self.free_params_names]], dtype=np.float64)
+        """fit.py:3448-3495: the log-posterior of one walker given as {name: value} (emcee with
+        ``parameter_names``, MAP).  A dict of equal-length arrays -- what emcee passes with
+        ``parameter_names`` AND ``vectorize=True`` -- gives the array of the walkers' values in one
+        device call."""
+        vals = [free_params_dict[n] for n in self.free_params_names]
+        if np.ndim(vals[0]) > 0:                                        # emcee vectorize=True
+            return self.log_probability_batch(np.stack([np.asarray(v, np.float64) for v in vals], axis=1))
+        row = np.array([vals], dtype=np.float64)
         if self.route == "device":
             return float(self._device()._eval(row)[0])
         return float(self._host_batch(row)[0])

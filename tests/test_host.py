@@ -142,3 +142,16 @@ def test_unsupported_uv_priors_raise():
     case["meta"] = m
     with pytest.raises(NotImplementedError):
         _posterior(case)
+
+
+def test_log_probability_dict_of_arrays_is_vectorised():
+    """emcee with parameter_names AND vectorize=True passes {name: array[W]}: the same values as
+    the batch form, one call."""
+    case = load_case("cfg2")
+    lpost = _posterior(case)
+    x = case["theta_free"]
+    d = {n: x[:, i] for i, n in enumerate(case["meta"]["free_names"])}
+    got = lpost.log_probability(d)
+    assert got.shape == (len(x),)
+    assert np.array_equal(got, lpost.log_probability_batch(x), equal_nan=True)
+    assert lpost.log_probability({n: float(v[0]) for n, v in d.items()}) == got[0] or np.isnan(got[0])
