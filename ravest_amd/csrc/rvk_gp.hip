@@ -945,6 +945,7 @@ unsigned gp_wave_blocks(long long n) {
 
 struct rvk_gp {
     rvk_handle *h = nullptr;
+    int device = -1;                         // the handle's, kept so destruction never dereferences h
     int mode = RVK_GP_FP64;                  // the reference's precision (fit.py:39)
     gp_launch_t launch = nullptr;
     unsigned grid = 0;           // concurrent walkers (one workgroup each)
@@ -969,7 +970,7 @@ static int gp_grow(double **p, size_t *cap, size_t need) { return grow_dev((void
 
 static void free_gp(rvk_gp *g) {
     if (!g) return;
-    if (g->h) (void)hipSetDevice(g->h->device);
+    if (g->device >= 0) (void)hipSetDevice(g->device);   // never through g->h: it may be gone already
     (void)hipFree(g->d_work);
     (void)hipFree(g->d_slots);
     (void)hipFree(g->d_work64);
@@ -1010,6 +1011,7 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     if (kernel != RVK_GP_QUASIPERIODIC) return fail(RVK_E_ARG, "unknown GP kernel type");
     if (h->n < 1 || h->n > RVK_GP_MAX_EPOCHS) return fail(RVK_E_ARG, "GP needs 1 <= n_epochs <= 4096");
     g->h = h;
+    g->device = h->device;
     HIPCHK(hipSetDevice(h->device));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, h->device));
@@ -1183,6 +1185,7 @@ int rvk_gp_predict(rvk_gp *g, const double *theta, const double *hyper, int64_t 
 
 struct rvk_gp_post {
     rvk_gp *g = nullptr;
+    int device = -1;               // the GP handle's, kept so destruction never dereferences g
     int n_free = 0, n_prior = 0, n_lp = 0, p_comb = 0;
     bool convert = false;
     double jac = 0.0, renorm = 0.0;
@@ -1207,7 +1210,7 @@ struct rvk_gp_post {
 
 static void free_gp_post(rvk_gp_post *p) {
     if (!p) return;
-    if (p->g) (void)hipSetDevice(p->g->h->device);
+    if (p->device >= 0) (void)hipSetDevice(p->device);   // never through p->g: it may be gone already
     (void)hipFree(p->d_colmap);
     (void)hipFree(p->d_tmpl);
     (void)hipFree(p->d_slots);
@@ -1289,6 +1292,7 @@ static int create_gp_post(rvk_gp_post *p, rvk_gp *g, int32_t n_free, const int32
         std::memcpy(slots[k].p, par + (size_t)k * RVK_PRIOR_NPAR, sizeof(double) * RVK_PRIOR_NPAR);
     }
     p->g = g;
+    p->device = g->h->device;
     p->n_free = n_free;
     p->n_prior = n_prior;
     p->n_lp = n_param_prior;

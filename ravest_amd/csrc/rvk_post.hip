@@ -96,6 +96,7 @@ unsigned wave_blocks(long long n) {
 
 struct rvk_post {
     rvk_handle *h = nullptr;
+    int device = -1;                       // the handle's, kept so destruction never dereferences h
     int n_free = 0, n_prior = 0;
     bool convert = false;
     bool fusable = false;                  // proposals can be made inside the likelihood kernel
@@ -186,7 +187,7 @@ static int ensure_graph(rvk_post *p, long long H, int steps) {
 
 static void free_post(rvk_post *p) {
     if (!p) return;
-    if (p->h) (void)hipSetDevice(p->h->device);
+    if (p->device >= 0) (void)hipSetDevice(p->device);   // never through p->h: it may be gone already
     (void)hipFree(p->d_colmap);
     (void)hipFree(p->d_tmpl);
     (void)hipFree(p->d_slots);
@@ -259,6 +260,7 @@ static int create_post(rvk_post *p, rvk_handle *h, int32_t n_free, const int32_t
         std::memcpy(slots[k].p, par + (size_t)k * RVK_PRIOR_NPAR, sizeof(double) * RVK_PRIOR_NPAR);
     }
     p->h = h;
+    p->device = h->device;
     p->n_free = n_free;
     p->n_prior = n_prior;
     p->convert = convert;

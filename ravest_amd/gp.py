@@ -26,6 +26,7 @@ the evidence corrections), with ``log_probability(dict)`` for emcee's
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from typing import Dict, List
 
 import numpy as np
@@ -340,7 +341,8 @@ class DeviceGPPosterior:
 
     def __init__(self, gpost: GPLogPosterior) -> None:
         pp = gpost._pp
-        self.gpost = gpost
+        self._gpost = weakref.ref(gpost)       # no cycle with GPLogPosterior._dpost (GC order)
+        self._gll = gpost.gp_log_likelihood    # the GP handle outlives this posterior
         names = pp._names
         pf = len(names)
         kinds, srcs, pars = [], [], []

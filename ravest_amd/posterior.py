@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import ctypes as C
 import logging
+import weakref
 from typing import Callable, Dict
 
 import numpy as np
@@ -328,7 +329,7 @@ class DevicePosterior:
     NotImplementedError (use ``LogPosterior.log_probability_batch``)."""
 
     def __init__(self, lpost: "LogPosterior") -> None:
-        self.lpost = lpost
+        self._lpost = weakref.ref(lpost)       # no cycle with LogPosterior._dpost (GC order)
         eng = lpost.log_likelihood.engine
         self.engine = eng
         names = lpost._names
