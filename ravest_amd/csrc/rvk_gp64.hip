@@ -292,7 +292,7 @@ struct Ops64 {
 // factors): summed over the 16 steps, the busiest SIMD's accumulation + S1 + S2 MFMAs drop from
 // 9312 to 8192 (of 6400 per SIMD if perfectly even).
 #ifndef RVK_GP64_BAL
-#define RVK_GP64_BAL 0
+#define RVK_GP64_BAL 1
 #endif
 template <int MAXR>
 struct RowMap {

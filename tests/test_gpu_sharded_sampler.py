@@ -84,7 +84,7 @@ def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2, gp=False):
     assert np.array_equal(got["nacc"], ref.naccepted)
     assert int(got["xbytes"]) == (W // 2) * 8
     assert got["nacc"].sum() > 0
-    assert np.array_equal(got["tau"], ref.get_autocorr_time(tol=0))
+    assert np.array_equal(got["tau"], ref.get_autocorr_time(tol=0), equal_nan=True)   # short chains: NaN tau
     for tag in ("even", "padded"):
         if f"post_{tag}" in got.files:
             assert np.array_equal(got[f"post_{tag}"], got[f"post_{tag}_ref"]), tag

@@ -18,7 +18,7 @@ fi
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 timeout -k 10 180 python tools/host_step_probe.py > $O/host_probe.json 2> $O/host_probe.err || { tail -20 $O/host_probe.err; exit 1; }
 cat $O/host_probe.json
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29561 bench.py --group --steps 20 --warmup 5 --no-cpu-baseline --no-gp --no-predictive > $O/bench_group.json 2> $O/bench_group.err || { tail -30 $O/bench_group.err; exit 1; }
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29561 --log-dir $O/tr_logs --redirects 3 --tee 3 bench.py --group --steps 20 --warmup 5 --no-cpu-baseline --no-gp --no-predictive > $O/bench_group.json 2> $O/bench_group.err || { tail -30 $O/bench_group.err; exit 1; }
 python -c "
 import json; d=json.load(open('$O/bench_group.json'))
 print('group', d.get('process_group'), 'value', d['value'], 'ranks_same', d['logprob_agreement']['ranks_bitwise_identical'])
