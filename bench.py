@@ -741,11 +741,7 @@ def main():
     eager_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))   # includes event/launch overhead
 
     # PCIe-inclusive host-buffer path (rvk_loglike: H2D theta, kernel, D2H), for DESIGN.md only
-    eng.loglike(theta)
-    th0 = time.perf_counter()
-    for _ in range(10):
-        eng.loglike(theta)
-    host_ms = (time.perf_counter() - th0) / 10 * 1e3
+    host_ms = _med_us(lambda: eng.loglike(theta), 200) * 1e-3     # median of 200 blocking calls
 
     # ---- the timed steps -------------------------------------------------------------------
     # graph (default): G-step HIP graphs replayed (S independent streams per graph); eager: K

@@ -149,10 +149,10 @@ def load() -> C.CDLL:
     L.rvk_gp_post_reserve.argtypes = [vp, C.c_int64]
     L.rvk_gp_logpost.argtypes = [vp, dp, C.c_int64, C.c_int64, dp]
     L.rvk_gp_logpost_device.argtypes = [vp, vp, C.c_int64, C.c_int64, vp, vp]
-    L.rvk_gp_stretch_run.argtypes = list(L.rvk_stretch_run.argtypes)
-    L.rvk_gp_stretch_draws.argtypes = list(L.rvk_stretch_draws.argtypes)
-    L.rvk_gp_stretch_propose.argtypes = list(L.rvk_stretch_propose.argtypes)
-    L.rvk_gp_stretch_update.argtypes = list(L.rvk_stretch_update.argtypes)
+    L.rvk_gp_stretch_run.argtypes = list(L.rvk_stretch_run.argtypes or ())
+    L.rvk_gp_stretch_draws.argtypes = list(L.rvk_stretch_draws.argtypes or ())
+    L.rvk_gp_stretch_propose.argtypes = list(L.rvk_stretch_propose.argtypes or ())
+    L.rvk_gp_stretch_update.argtypes = list(L.rvk_stretch_update.argtypes or ())
     for name in ("rvk_gp_loglike", "rvk_gp_loglike_device", "rvk_gp_set_precision", "rvk_gp_predict",
                  "rvk_gp_predict_device", "rvk_gp_post_reserve", "rvk_gp_logpost", "rvk_gp_logpost_device",
                  "rvk_gp_stretch_run", "rvk_gp_stretch_draws", "rvk_gp_stretch_propose", "rvk_gp_stretch_update",

@@ -646,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restric
                                                          unsigned long long sel, const SC *__restrict__ gtab,
                                                          double *__restrict__ out) {
     __shared__ SC tab[kTabN];
-    __shared__ PlanetK pkl[NP == 0 ? kWavesPerBlock : 1][NP == 0 ? RVK_MAX_PLANETS : 1];
+    __shared__ PlanetK pkl[kWavesPerBlock][NP == 0 ? RVK_MAX_PLANETS : NP];
     load_tab(tab, gtab);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -655,26 +655,21 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restric
     const int nsel = __builtin_popcountll(sel);
     for (long long s = wave0; s < n_samples; s += nwaves) {
         const double *row = theta + s * stride;
+        // lane q < nsel: the q-th selected planet (q-th set bit of `sel`), written straight into
+        // LDS by the out-of-line conversion (a PlanetK on the stack would be 64 B/lane of scratch
+        // stores per sample -- half the output's bytes again in WRITE_SIZE)
+        int okq = 1;
+        if (lane < nsel) {
+            unsigned long long m = sel;
+            for (int k = 0; k < lane; ++k) m &= m - 1ull;
+            okq = planet_consts_lds(par, row + 5 * __builtin_ctzll(m), &pkl[wv][lane]);
+        }
+        const bool ok = __builtin_amdgcn_ballot_w64(!okq) == 0;
+        wave_lds_sync();
         PlanetK pk[NP > 0 ? NP : 1];
-        bool ok = true;
         if constexpr (NP > 0) {
 #pragma unroll
-            for (int q = 0; q < NP; ++q) {   // q-th selected planet = q-th set bit of `sel`
-                unsigned long long m = sel;
-                for (int k = 0; k < q; ++k) m &= m - 1ull;
-                ok &= planet_consts(par, row + 5 * __builtin_ctzll(m), pk[q]);
-            }
-        } else {                             // lane q < nsel: the q-th selected planet, into LDS
-            int okq = 1;
-            if (lane < nsel) {
-                unsigned long long m = sel;
-                for (int k = 0; k < lane; ++k) m &= m - 1ull;
-                PlanetK q;
-                okq = planet_consts(par, row + 5 * __builtin_ctzll(m), q);
-                pkl[wv][lane] = q;
-            }
-            ok = __builtin_amdgcn_ballot_w64(!okq) == 0;
-            wave_lds_sync();
+            for (int q = 0; q < NP; ++q) pk[q] = pkl[wv][q];
         }
         const double *g = row + 5 * n_planets_total;
         const double *jit = g + n_inst;
@@ -695,7 +690,7 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(const double *__restric
             if (what & RVK_PRED_GAMMA) v += g[iq ? iq[j] : 0];
             out[s * n_t + j] = ok ? v : NAN;
         }
-        if constexpr (NP == 0) wave_lds_sync();   // pkl is rewritten for the wave's next sample
+        wave_lds_sync();   // pkl is rewritten for the wave's next sample
     }
 }
 

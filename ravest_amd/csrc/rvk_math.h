@@ -494,6 +494,16 @@ __device__ __attribute__((noinline)) bool planet_consts(int par, const double *p
     return planet_consts_t<-1>(p5, pk, par);
 }
 
+// The same, storing into an LDS slot through a shared-address-space pointer (no caller stack
+// object: the posterior predictive's per-sample prep, one planet per lane; dst is an LDS slot).
+__device__ __attribute__((noinline)) bool planet_consts_lds(int par, const double *p5,
+                                                            PlanetK *dst) {
+    PlanetK pk;
+    const bool ok = planet_consts_t<-1>(p5, pk, par);
+    *dst = pk;
+    return ok;
+}
+
 // One planet's RV at time t (model.py:327, 119-121, 170).  e == 0 takes the
 // same arithmetic (the solvers return E = M), so there is no branch.
 template <int SOLVER>

@@ -32,13 +32,22 @@ def main():
     tq = torch.linspace(0.0, 1000.0, T, dtype=torch.float64, device="cuda")
     out = torch.empty((S, T), dtype=torch.float64, device="cuda")
     out2 = torch.empty((S, 1024), dtype=torch.float64, device="cuda")
-    for _ in range(3):
-        eng.predict_device(th, tq, out)
-        out.fill_(1.0)
-        out2.fill_(2.0)
+    out3 = torch.empty((S, 2048), dtype=torch.float64, device="cuda")
+    tq2 = torch.linspace(0.0, 1000.0, 1024, dtype=torch.float64, device="cuda")
+    cases = [  # label, bytes written, fn -- each run 3 times back to back, in this order
+        ("predict T=1000 (rows 8000 B, 8 B/lane)", S * T * 8, lambda: eng.predict_device(th, tq, out)),
+        ("predict T=1024 (rows 8192 B, 8 B/lane)", S * 1024 * 8, lambda: eng.predict_device(th, tq2, out2)),
+        ("fill [S,1000] contiguous (vectorised)", S * T * 8, lambda: out.fill_(1.0)),
+        ("fill [S,1024] contiguous (vectorised)", S * 1024 * 8, lambda: out2.fill_(2.0)),
+        ("fill [S,:999] of [S,1000] (8 B/lane, rows 8000 B)", S * 999 * 8, lambda: out[:, :999].fill_(3.0)),
+        ("fill [S,:1024] of [S,2048] (8 B/lane, rows aligned)", S * 1024 * 8, lambda: out3[:, :1024].fill_(4.0)),
+    ]
     torch.cuda.synchronize()
-    print(json.dumps({"S": S, "T": T, "predict_bytes": S * T * 8, "fill_bytes": S * T * 8,
-                      "fill1024_bytes": S * 1024 * 8, "dispatches_each": 3}))
+    for _, _, fn in cases:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+    print(json.dumps({"S": S, "T": T, "reps": 3, "cases": [[c[0], c[1]] for c in cases]}))
 
 
 if __name__ == "__main__":
