@@ -228,10 +228,27 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
         // prep (the table fill above lands under the same barrier)
         if constexpr (!FUSE) {
-        for (int k = threadIdx.x; k < nb * np; k += BLK) {
-            const int j = k / np, p = k - j * np;
-            const long long w = base + j;
-            const double *p5 = theta + w * stride + 5 * p;
+        static_assert(WB * NPA <= BLK, "the prep gives each thread at most one (walker, planet)");
+        const int k = threadIdx.x;
+        const bool has = k < nb * np;
+        const int j = has ? k / np : 0, p = has ? k - j * np : 0;
+        const double *p5 = theta + (base + j) * stride + 5 * p;
+        if constexpr (TP && RVK_PREP_TAB && RVK_TAB_LDS) {
+            // "P K e w Tp" inline; its sin/cos(w) reads the LDS table that all waves fill: the row
+            // is loaded first, then the block barrier publishes the table (the first pass; later
+            // passes follow the end-of-pass barrier), so the two loads' latencies overlap
+            double r5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+            if (has) {
+#pragma unroll
+                for (int c = 0; c < 5; ++c) r5[c] = p5[c];
+            }
+            if (base == (long long)blockIdx.x * wb) __syncthreads();
+            if (has) {
+                PlanetK pk;
+                okp[j][p] = planet_consts_t<0, true>(r5, pk, 0, tab);
+                pks[j][p] = pk;
+            }
+        } else if (has) {
             PlanetK pk;
             // "P K e w Tp" inline (no call, no scratch); the others out of line
             const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
@@ -511,13 +528,29 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);
-        for (int k = threadIdx.x; k < nb * NP; k += kBlock) {
-            const int j = k / NP, p = k - j * NP;
-            const double *p5 = theta + (base + j) * stride + 5 * p;
+        static_assert(WB * NP <= kBlock, "the prep gives each thread at most one (walker, planet)");
+        const int k = threadIdx.x;
+        const bool has = k < nb * NP;
+        const int jp = has ? k / NP : 0, pp = has ? k - jp * NP : 0;
+        const double *p5 = theta + (base + jp) * stride + 5 * pp;
+        if constexpr (TP && RVK_PREP_TAB) {
+            // as in loglike_kernel: the row first, then the barrier that publishes the LDS table
+            double r5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+            if (has) {
+#pragma unroll
+                for (int c = 0; c < 5; ++c) r5[c] = p5[c];
+            }
+            if (base == (long long)blockIdx.x * wb) __syncthreads();
+            if (has) {
+                PlanetK pk;
+                okp[jp][pp] = planet_consts_t<0, true>(r5, pk, 0, tab);
+                pks[jp][pp] = pk;
+            }
+        } else if (has) {
             PlanetK pk;
             const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
-            pks[j][p] = pk;
-            okp[j][p] = ok;
+            pks[jp][pp] = pk;
+            okp[jp][pp] = ok;
         }
         __syncthreads();
         for (int j0 = wv * SEG; j0 < nb; j0 += kWavesPerBlock * SEG) {

@@ -192,6 +192,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
 #endif
     for (int i = tid; i < kTabN; i += NT) L.tab[i] = d.tab[i];
     for (int i = tid; i < nt * nt; i += NT) L.slot[i] = slots[i];
+    __syncthreads();   // the table is read by the planet prep below (threads < np), before any other barrier
     float *A = work + (long long)blockIdx.x * work_stride;
 
     for (long long w = blockIdx.x; w < W; w += gridDim.x) {

@@ -423,6 +423,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     const EpochData &d = a.d;
     const bool multi = ni > 1, tp = d.par == RVK_PAR_PKEWTP;
     for (int i = tid; i < kTabN; i += NT) tab[i] = d.tab[i];
+    __syncthreads();   // the table is read by the planet prep below (threads < np), before any other barrier
     double *wk = a.work + (long long)blockIdx.x * a.work_stride;
 
     for (long long w = blockIdx.x; w < a.W; w += gridDim.x) {
