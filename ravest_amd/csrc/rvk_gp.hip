@@ -72,7 +72,7 @@ namespace {
 #define RVK_GP_RPASS 2    // rows per accumulation pass (the A tiles are re-read once per pass)
 #endif
 #ifndef RVK_GP_SCHEDB
-#define RVK_GP_SCHEDB 0   // scheduling barriers around each ring set's loads and MFMAs (fp64: see rvk_gp64.hip)
+#define RVK_GP_SCHEDB 1   // scheduling barriers around each ring set's loads and MFMAs (measured 3.21-3.26 vs 3.28-3.29 ms without; fp64: see rvk_gp64.hip)
 #endif
 #ifndef RVK_GP_NBUF
 #define RVK_GP_NBUF 2     // operand register sets in the ring (NBUF - 1 in flight)
