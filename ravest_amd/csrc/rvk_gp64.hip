@@ -47,7 +47,8 @@ namespace {
 
 #ifndef RVK_GP64_ABLATE
 #define RVK_GP64_ABLATE 0 // timing experiments only (wrong results): 1 A tiles, 2 B tiles of the accumulation from tile j = 0,
-                          // 4 no diagonal factor, 8 no accumulation MFMAs (loads kept)
+                          // 4 no diagonal factor, 8 no accumulation MFMAs (loads kept), 16 no covariance
+                          // function (tau / 2 instead of the QP kernel)
 #endif
 #ifndef RVK_GP64_TRACE
 #define RVK_GP64_TRACE 0  // timing experiments only: s_memtime per phase, first walker of block 0
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int gj = bj * TB + 16 * p + (lane >> 4) + 4 * i;
-                        const double kv = qp_cov(h, ti - Lt[gj]);
+                        const double kv = (RVK_GP64_ABLATE & 16) ? 0.5 * (ti - Lt[gj]) : qp_cov(h, ti - Lt[gj]);
                         const bool in = gi < n && gj < n, dg = gi == gj;
                         const double v = in ? (dg ? kv + di : kv) : (dg ? 1.0 : 0.0);
                         A.c[p][q][i] = -v;

@@ -9,3 +9,4 @@ for rep in 1 2 3; do timeout -k 10 200 python tools/kbench.py > $O/kb/kb_librvk_
 python tools/ab_summary.py $O/kb
 timeout -k 10 300 python tools/gp_bench.py 4096 512 fp64 > $O/gp64.json 2>&1 && timeout -k 10 300 python tools/gp_bench.py 4096 512 fp32+fp64 > $O/gp32.json 2>&1 || exit 1
 tail -1 $O/gp64.json | cut -c1-200; tail -1 $O/gp32.json | cut -c1-200
+SKIPTEST=1 bash tools/gp64_ab.sh ${TAG}_abl fp64 || exit 1
