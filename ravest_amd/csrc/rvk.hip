@@ -47,6 +47,9 @@ namespace {
 #ifndef RVK_TP_INLINE
 #define RVK_TP_INLINE 1               // "P K e w Tp": inline conversion in the prep (1) or the out-of-line one (0)
 #endif
+#ifndef RVK_PREP_GTAB
+#define RVK_PREP_GTAB 0               // loglike prep's sin/cos(w) from the global table (1) or the LDS one behind a barrier (0)
+#endif
 #ifndef RVK_EPOCH_OFF32
 #define RVK_EPOCH_OFF32 1             // epoch loads through one 32-bit byte offset (global_load saddr form)
 #endif
@@ -233,7 +236,13 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const bool has = k < nb * np;
         const int j = has ? k / np : 0, p = has ? k - j * np : 0;
         const double *p5 = theta + (base + j) * stride + 5 * p;
-        if constexpr (TP && RVK_PREP_TAB && RVK_TAB_LDS) {
+        if constexpr (TP && RVK_PREP_TAB && RVK_TAB_LDS && RVK_PREP_GTAB) {
+            if (has) {   // sin/cos(w) from the global (L2-resident) table: no barrier before the prep
+                PlanetK pk;
+                okp[j][p] = planet_consts_t<0, true>(p5, pk, 0, d.tab);
+                pks[j][p] = pk;
+            }
+        } else if constexpr (TP && RVK_PREP_TAB && RVK_TAB_LDS) {
             // "P K e w Tp" inline; its sin/cos(w) reads the LDS table that all waves fill: the row
             // is loaded first, then the block barrier publishes the table (the first pass; later
             // passes follow the end-of-pass barrier), so the two loads' latencies overlap

@@ -1024,6 +1024,7 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     g->cond64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, true, s64);
     if (!g->launch64 || !g->cond64) return fail(RVK_E_ARG, "GP supports 1..32 planets");
     g->lds64 = gp64_lds_bytes(h->n, h->n_planets, s64.nw);
+    if (g->lds64 > (size_t)160 * 1024) return fail(RVK_E_ARG, "GP fp64 kernel: LDS need exceeds 160 KB");
     g->grid64 = (unsigned)prop.multiProcessorCount;
     g->w64stride = gp64_work_doubles(h->n);
     HIPCHK(hipMalloc(&g->d_work64, sizeof(double) * (size_t)g->w64stride * g->grid64));
