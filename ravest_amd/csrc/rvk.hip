@@ -48,7 +48,8 @@ namespace {
 #define RVK_TP_INLINE 1               // "P K e w Tp": inline conversion in the prep (1) or the out-of-line one (0)
 #endif
 #ifndef RVK_PREP_GTAB
-#define RVK_PREP_GTAB 0               // loglike prep's sin/cos(w) from the global table (1) or the LDS one behind a barrier (0)
+#define RVK_PREP_GTAB 1               // prep's sin/cos(w) from the global (L2) table (1), or from the LDS copy behind an
+                                      // extra block barrier (0): measured 7.4 vs 7.7 us on config 2
 #endif
 #ifndef RVK_EPOCH_OFF32
 #define RVK_EPOCH_OFF32 1             // epoch loads through one 32-bit byte offset (global_load saddr form)
@@ -542,7 +543,13 @@ __global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int
         const bool has = k < nb * NP;
         const int jp = has ? k / NP : 0, pp = has ? k - jp * NP : 0;
         const double *p5 = theta + (base + jp) * stride + 5 * pp;
-        if constexpr (TP && RVK_PREP_TAB) {
+        if constexpr (TP && RVK_PREP_TAB && RVK_PREP_GTAB) {
+            if (has) {   // sin/cos(w) from the global table (the LDS copy is not yet published)
+                PlanetK pk;
+                okp[jp][pp] = planet_consts_t<0, true>(p5, pk, 0, d.tab);
+                pks[jp][pp] = pk;
+            }
+        } else if constexpr (TP && RVK_PREP_TAB) {
             // as in loglike_kernel: the row first, then the barrier that publishes the LDS table
             double r5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
             if (has) {

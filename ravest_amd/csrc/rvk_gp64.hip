@@ -202,8 +202,11 @@ __device__ __forceinline__ double exp_nonpos(double x) {
 // value drops the (-1)^k signs of the reduction.  Same absolute error as the direct form (t_i - t_0
 // is exact for dates of one magnitude; host check on config 5: 1.7e-14 vs 1.4e-14 max abs error
 // in sin^2 against 40-digit values), 10 fewer fp64 instructions per covariance element.
+#ifndef RVK_GP64_COVSB
+#define RVK_GP64_COVSB 1     // scheduling barrier after each covariance element (register pressure)
+#endif
 #ifndef RVK_GP64_SINADD
-#define RVK_GP64_SINADD 1
+#define RVK_GP64_SINADD 0
 #endif
 __device__ __forceinline__ double sinpi_red(double r) {    // sin(pi r), |r| <= 1/2 (sinpi_sq's fit)
     const double r2 = r * r;
@@ -557,8 +560,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                     for (int p = 0; p < 2; ++p)
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
+                        for (int i = 0; i < 4; ++i) {
                             A.c[p][q][i] = -kval(ti, si, ci, bj * TB + 16 * p + (lane >> 4) + 4 * i);
+                            if (RVK_GP64_COVSB) __builtin_amdgcn_sched_barrier(0);   // one element at a time
+                        }
                 }
                 return;
             }
