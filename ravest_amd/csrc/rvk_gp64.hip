@@ -334,7 +334,7 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
 // compiler from sinking the loads next to their MFMAs (which left every quarter's load latency
 // exposed: the accumulation ran at ~40 % of the matrix pipe, profiles/round2/gp64_phase_trace.txt).
 #ifndef RVK_GP64_RING
-#define RVK_GP64_RING 3
+#define RVK_GP64_RING 2   // operand register sets (round 4: 6.24-6.34 ms vs 6.40-6.46 with 3, after the other changes)
 #endif
 template <int R>
 struct Ops64 {
