@@ -5,9 +5,10 @@
 set -e
 OUT=${1:-gpurun_out/pmc}
 CFG=${2:-2}
+KF=${3:-}          # kernel-name filter (default: the plain loglike launch with the most dispatches)
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-sampler --no-gp --no-predictive --no-configs"
+CMD="python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-sampler --no-gp --no-predictive --no-configs --no-host-path"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_WAVES" \
@@ -17,4 +18,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- $CMD > $OUT/p$i.log 2>&1
 done
-python tools/pmc_summary.py $OUT $CFG "" "$CMD"
+python tools/pmc_summary.py $OUT $CFG "$KF" "$CMD"
+rm -rf $OUT/p[0-9]*/   # raw per-dispatch CSVs (tens of MB): the summary is what is kept

@@ -19,3 +19,4 @@ done
 # the fp64 MFMA op counter in a pass of its own (optional: skipped if this ROCm lacks it)
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 --output-format csv -d $OUT/p9 -o run -- $CMD > $OUT/p9.log 2>&1 || true
 python tools/pmc_summary.py $OUT $LABEL $KF "$CMD"
+rm -rf $OUT/p[0-9]*/
