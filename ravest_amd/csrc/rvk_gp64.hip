@@ -202,6 +202,9 @@ __device__ __forceinline__ double exp_nonpos(double x) {
 // value drops the (-1)^k signs of the reduction.  Same absolute error as the direct form (t_i - t_0
 // is exact for dates of one magnitude; host check on config 5: 1.7e-14 vs 1.4e-14 max abs error
 // in sin^2 against 40-digit values), 10 fewer fp64 instructions per covariance element.
+#ifndef RVK_GP64_KILLACC
+#define RVK_GP64_KILLACC 1   // zero the accumulator slots at each step start (ends their live ranges)
+#endif
 #ifndef RVK_GP64_COVSB
 #define RVK_GP64_COVSB 0     // scheduling barrier after each covariance element (measured 6.43 vs 6.54 ms without)
 #endif
@@ -660,6 +663,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
             for (int k = 0; k < nt; ++k) {
                 G64_MARK(k, 0);
                 G64_MARK(k, 1);
+                if (RVK_GP64_KILLACC) {
+                    // every live slot is re-formed from the covariance below and the previous step's
+                    // values were parked by S2: ending their live ranges here keeps the compiler from
+                    // carrying all MAXR accumulators (and spilling them) across the whole step
+#pragma unroll
+                    for (int q = 0; q < MAXR; ++q)
+#pragma unroll
+                        for (int p = 0; p < 2; ++p)
+#pragma unroll
+                            for (int qq = 0; qq < 2; ++qq) nacc[q].c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
+                }
                 for (int qo = 0; qo < (grouped ? nown : 1) && k + 1 < nt; qo += MAXR) {   // one trip unless grouped
                     if (grouped && wr + NA * (qo + MAXR - 1) < k + 1) continue;    // the group's rows are finished
 #pragma unroll
