@@ -47,6 +47,9 @@ namespace {
 #ifndef RVK_TP_INLINE
 #define RVK_TP_INLINE 1               // "P K e w Tp": inline conversion in the prep (1) or the out-of-line one (0)
 #endif
+#ifndef RVK_FUSE_COMPOSE
+#define RVK_FUSE_COMPOSE 1            // fused prep: planet / prior / jitter operands straight from q (composed column map)
+#endif
 #ifndef RVK_PREP_GTAB
 #define RVK_PREP_GTAB 1               // prep's sin/cos(w) from the global (L2) table (1), or from the LDS copy behind an
                                       // extra block barrier (0): measured 7.4 vs 7.7 us on config 2
@@ -297,19 +300,31 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     if (fc < 0) fv = ftm[lane];
                     ff[j][lane] = fv;
                 }
+                // column c of the full row, per lane: RVK_FUSE_COMPOSE reads it from q through the
+                // composed map (one bpermute level on the chain to the planet constants and the
+                // priors instead of q -> row -> operand); same values as reading the row fv
+                auto col = [&](int c) -> double {
+                    if constexpr (RVK_FUSE_COMPOSE) {
+                        const int m = fcol[c];
+                        const double v = shfl_d(q_s, m < 0 ? 0 : m);
+                        return m < 0 ? ftm[c] : v;
+                    } else {
+                        return shfl_d(fv, c);
+                    }
+                };
                 const int ioff = 5 * pd.n_planets + pd.n_inst;
-                const double jv = shfl_d(fv, ioff + (lane < pd.n_inst ? lane : 0));
+                const double jv = col(ioff + (lane < pd.n_inst ? lane : 0));
                 bool dead0 = lane < pd.n_inst && jv < 0.0;                                    // fit.py:3465-3468
                 double term = 0.0;
                 {
                     const int pl = lane < NP ? lane : 0;
                     double p5[5];
 #pragma unroll
-                    for (int k = 0; k < 5; ++k) p5[k] = shfl_d(fv, 5 * pl + k);
+                    for (int k = 0; k < 5; ++k) p5[k] = col(5 * pl + k);
                     // the prior-side conversion (Case 3, fit.py:3418-3446): lane p < NP converts
                     // planet p; a ValueError rejects the walker; a slot with src < 0 reads it
                     const int src = lane < pd.n_prior ? fsl[lane].src : 0;
-                    double xv = shfl_d(fv, src < 0 ? 0 : src);
+                    double xv = col(src < 0 ? 0 : src);
                     if constexpr (EXT) {
                         double d5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
                         if (CONV && lane < NP) dead0 |= !to_default_call(pd.par, p5, d5);
