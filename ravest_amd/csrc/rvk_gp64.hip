@@ -209,7 +209,7 @@ __device__ __forceinline__ double exp_nonpos(double x) {
 #define RVK_GP64_COVSB 0     // scheduling barrier after each covariance element (measured 6.43 vs 6.54 ms without)
 #endif
 #ifndef RVK_GP64_SINADD
-#define RVK_GP64_SINADD 0
+#define RVK_GP64_SINADD 1
 #endif
 __device__ __forceinline__ double sinpi_red(double r) {    // sin(pi r), |r| <= 1/2 (sinpi_sq's fit)
     const double r2 = r * r;
