@@ -45,7 +45,8 @@ namespace {
 #define RVK_GP_WGPCU 2    // concurrent workgroups per CU (each its own workspace), LDS permitting
 #endif
 #ifndef RVK_GP_ABLATE
-#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 part1 operands from LDS, 2 no factor
+#define RVK_GP_ABLATE 0   // timing experiments only (wrong results): 1 part1 operands from LDS, 2 no factor,
+                          // 4 no covariance function, 8 no accumulation MFMAs
 #endif
 #ifndef RVK_GP_PRIO
 #define RVK_GP_PRIO 1     // s_setprio of the factoring wave (1 and 3 measured equal, 0 within noise)
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                 for (int e = 0; e < 4; ++e) {
                     const float sn = __builtin_amdgcn_sinf(0.5f * (ui - ujv[e]));   // v_sin_f32: revolutions
                     const float x = si - sjv[e];
-                    t[4 * u + e] = namp2 * __expf(-(gam * (sn * sn) + 0.5f * (x * x)));
+                    t[4 * u + e] = (RVK_GP_ABLATE & 4) ? 0.5f * x : namp2 * __expf(-(gam * (sn * sn) + 0.5f * (x * x)));
                 }
             }
             if (bi == bj || (bi + 1) * TB > n || (bj + 1) * TB > n) {
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
                         for (int b = 0; b < NB; ++b) {
                             issue(ring[(b + NB - 1) % NB], hx + b + NB - 1);
                             if (RVK_GP_SCHEDB) __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead
-                            if (b == 0 || hx + b < H1) consume(ring[b], hx + b);
+                            if ((b == 0 || hx + b < H1) && !(RVK_GP_ABLATE & 8)) consume(ring[b], hx + b);
                             if (RVK_GP_SCHEDB) __builtin_amdgcn_sched_barrier(0);
                         }
                     }
