@@ -47,6 +47,9 @@ namespace {
 #ifndef RVK_TP_INLINE
 #define RVK_TP_INLINE 1               // "P K e w Tp": inline conversion in the prep (1) or the out-of-line one (0)
 #endif
+#ifndef RVK_SEG_LB3
+#define RVK_SEG_LB3 4                 // min blocks per CU of the segmented kernel for NP >= 3 (4: <= 128 VGPRs)
+#endif
 #ifndef RVK_FUSE_COMPOSE
 #define RVK_FUSE_COMPOSE 0            // fused prep: operands straight from q by the composed column map (1): measured 18.4 vs 17.9 us per step, off
 #endif
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
 // same, lanes stride their walker's epochs by LPW; each segment is summed with the row
 // butterflies and v_readlane of its rows.
 template <int NP, bool MULTI, bool TP, int LPW>
-__global__ __launch_bounds__(kBlock, 4) void loglike_seg_kernel(EpochData d, int n_epochs, int n_inst,
+__global__ __launch_bounds__(kBlock, (NP >= 3 ? RVK_SEG_LB3 : 4)) void loglike_seg_kernel(EpochData d, int n_epochs, int n_inst,
                                                                  const double *__restrict__ theta,
                                                                  long long n_walkers, long long stride, int wb,
                                                                  double *__restrict__ out, PostArgs post) {
