@@ -9,3 +9,6 @@ for rep in 1 2 3; do
   done
 done
 python tools/ab_summary.py $O/kb
+RAVEST_AMD_LIB=$(realpath varlib/trace/librvk_lltrace.so) timeout -k 10 120 python tools/sampler_trace.py 4096 > $O/sampler_trace.txt 2>&1 || { tail -5 $O/sampler_trace.txt; exit 1; }
+RAVEST_AMD_LIB=$(realpath varlib/trace/librvk_lltrace.so) timeout -k 10 120 python tools/ll_trace.py 4096 > $O/ll_trace.txt 2>&1 || { tail -5 $O/ll_trace.txt; exit 1; }
+cat $O/sampler_trace.txt $O/ll_trace.txt
