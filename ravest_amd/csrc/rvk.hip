@@ -50,6 +50,9 @@ namespace {
 #ifndef RVK_SEG_LB3
 #define RVK_SEG_LB3 4                 // min blocks per CU of the segmented kernel for NP >= 3 (4: <= 128 VGPRs)
 #endif
+#ifndef RVK_FUSE_PROLOGUE
+#define RVK_FUSE_PROLOGUE 1           // fused kernel prologue: loads first, LDS stores after (see loglike_kernel)
+#endif
 #ifndef RVK_FUSE_COMPOSE
 #define RVK_FUSE_COMPOSE 0            // fused prep: operands straight from q by the composed column map (1): measured 18.4 vs 17.9 us per step, off
 #endif
@@ -176,9 +179,22 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         t_1 = d.t[lane]; v_1 = d.vel[lane]; s_1 = d.s2[lane];
         if (MULTI) i_1 = d.inst[lane];
     }
+    // FUSE (RVK_FUSE_PROLOGUE): the table fill and the posterior constants are loaded into
+    // registers first and stored to LDS only after the walker's draw / row loads are issued, so
+    // the prologue is three memory round trips (constants and draws || rows || barrier), not a
+    // chain of a wait per kind of load
+    constexpr bool TDEF = FUSE && RVK_FUSE_PROLOGUE && RVK_TAB_LDS && BLK >= kTabN;
 #if RVK_TAB_LDS
     __shared__ SC tab[kTabN];
-    for (int i = threadIdx.x; i < kTabN; i += BLK) tab[i] = d.tab[i];
+    double tab_s = 0.0, tab_c = 0.0;   // (scalars: a struct here is promoted to a per-thread LDS copy)
+    if constexpr (TDEF) {
+        if (threadIdx.x < kTabN) {
+            tab_s = d.tab[threadIdx.x].s;
+            tab_c = d.tab[threadIdx.x].c;
+        }
+    } else {
+        for (int i = threadIdx.x; i < kTabN; i += BLK) tab[i] = d.tab[i];
+    }
 #else
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
 #endif
@@ -204,32 +220,88 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             f.a = lane < D ? sa.q[w * sa.qstride + lane] : 0.0;
             return f;
         }
-        const RunArgs &run = *sa.run;
         const long long j = sa.j0 + w;   // global proposal index within the half
-        const PreDraw p = sa.pre[((long long)sa.step * 2 + sa.half) * sa.hfull + j];
-        f.s = p.s;
-        f.c = p.c;
-        f.z = p.z;
-        f.fac = p.fac;
-        f.lau = p.lau;
-        f.lpo = ACCEPT ? run.lp[p.s] : 0.0;
-        f.nacc = (ACCEPT && run.nacc) ? run.nacc[p.s] : 0;
+        const PreDraw *pp = sa.pre + ((long long)sa.step * 2 + sa.half) * sa.hfull + j;
+        // every scalar load of the fetch (the draw, the state pointers) issued before any is used:
+        // one wait for all of them instead of a wait per load
+        const long long ps = pp->s, pc = pp->c;
+        const double pz = pp->z, pfac = pp->fac, plau = pp->lau;
+        using gdp = const __attribute__((address_space(1))) double *;   // global loads (a flat one holds lgkmcnt)
+        const gdp rx = (gdp)sa.run->x;
+        const gdp rlp = (gdp)sa.run->lp;
+        const __attribute__((address_space(1))) long long *const rnacc =
+            (const __attribute__((address_space(1))) long long *)sa.run->nacc;
+        if (RVK_FUSE_PROLOGUE) __builtin_amdgcn_sched_barrier(0);
+        f.s = ps;
+        f.c = pc;
+        f.z = pz;
+        f.fac = pfac;
+        f.lau = plau;
+        // the rows first, then the walker's log-prob and count: all four loads in flight together
         f.a = f.b = 0.0;
         if (lane < D) {
-            f.a = run.x[p.s * D + lane];
-            f.b = run.x[p.c * D + lane];
+            f.a = rx[ps * D + lane];
+            f.b = rx[pc * D + lane];
         }
+        f.lpo = ACCEPT ? rlp[ps] : 0.0;
+        f.nacc = (ACCEPT && rnacc) ? rnacc[ps] : 0;
         return f;
     };
     Fetch pre{};
+    int pf_draw = 0;   // a word of the next half-step's draw row, touched so it is L2-resident then
     if constexpr (FUSE) {
         const long long w0 = (long long)blockIdx.x * wb + wv;
-        if (wv < wb && w0 < n_walkers) pre = fetch(w0);
-        for (int i = threadIdx.x; i < sa.pd.p_full; i += BLK) {
-            fcol[i] = sa.pd.colmap[i];
-            ftm[i] = sa.pd.tmpl[i];
+        if constexpr (ACCEPT && !DIRECT) {
+            // the same block index runs on the same XCD in the next launch of this grid
+            if (sa.pre_next && wv < wb && w0 < n_walkers && lane == 0) {
+                int zo = 0;
+                asm volatile("" : "+v"(zo));   // a VGPR offset: a vector load, off the scalar waits
+                pf_draw = *(const __attribute__((address_space(1))) int *)(
+                    reinterpret_cast<const char *>(sa.pre_next + sa.j0 + w0) + zo);   // global_load, not flat
+            }
         }
-        for (int i = threadIdx.x; i < sa.pd.n_prior; i += BLK) fsl[i] = sa.pd.slots[i];
+        if constexpr (RVK_FUSE_PROLOGUE) {
+            static_assert(BLK >= kFuseMaxPFull && BLK >= kFuseMaxPrior, "one staging entry per thread");
+            const int tid = threadIdx.x;
+            const bool stc = tid < sa.pd.p_full, sts = tid < sa.pd.n_prior;
+            int fc_r = 0;
+            double ftm_r = 0.0;
+            constexpr int SW = sizeof(PriorSlot) / 8;   // the slot as 8-byte words, in registers
+            static_assert(sizeof(PriorSlot) % 8 == 0, "PriorSlot is whole 8-byte words");
+            unsigned long long sw_r[SW];
+            if (stc) {
+                fc_r = sa.pd.colmap[tid];
+                ftm_r = sa.pd.tmpl[tid];
+            }
+            if (sts) {
+                const unsigned long long *src = reinterpret_cast<const unsigned long long *>(sa.pd.slots + tid);
+#pragma unroll
+                for (int k = 0; k < SW; ++k) sw_r[k] = src[k];
+            }
+            if (wv < wb && w0 < n_walkers) pre = fetch(w0);
+            __builtin_amdgcn_sched_barrier(0);   // the stores below wait for their loads only
+#if RVK_TAB_LDS
+            if constexpr (TDEF) {
+                if (tid < kTabN) tab[tid] = SC{tab_s, tab_c};
+            }
+#endif
+            if (stc) {
+                fcol[tid] = fc_r;
+                ftm[tid] = ftm_r;
+            }
+            if (sts) {
+                unsigned long long *dst = reinterpret_cast<unsigned long long *>(fsl + tid);
+#pragma unroll
+                for (int k = 0; k < SW; ++k) dst[k] = sw_r[k];
+            }
+        } else {
+            if (wv < wb && w0 < n_walkers) pre = fetch(w0);
+            for (int i = threadIdx.x; i < sa.pd.p_full; i += BLK) {
+                fcol[i] = sa.pd.colmap[i];
+                ftm[i] = sa.pd.tmpl[i];
+            }
+            for (int i = threadIdx.x; i < sa.pd.n_prior; i += BLK) fsl[i] = sa.pd.slots[i];
+        }
         __syncthreads();   // (also publishes the table)
     }
     LL_MARK(0);
@@ -526,6 +598,10 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // LDS rows are rewritten next pass
     }
     LL_MARK(7);
+    if constexpr (FUSE && ACCEPT && !DIRECT) {   // a use of the prefetched word (a no-op if it ever fires)
+        asm volatile("" : "+v"(pf_draw));   // the word is consumed here, at the end, not earlier
+        if (pf_draw == 0x7fc0dead && lane == 0) atomicOr(sa.run->status, 0);
+    }
 }
 
 // Segmented variant: LPW lanes per walker, SEG = 64 / LPW walkers per wave (production

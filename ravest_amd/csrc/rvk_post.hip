@@ -130,7 +130,7 @@ struct rvk_post {
 // accepted inside the likelihood kernel (fused path), or propose_kernel + the likelihood with
 // the accept / reject fused in (production solver), or + stretch_accept_kernel (reference solver).
 static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long j0, long long count,
-                         long long hfull, const PreDraw *pre) {
+                         long long hfull, const PreDraw *pre, const PreDraw *pre_next = nullptr) {
     rvk_handle *h = p->h;
     const PostDev pd = p->dev();
     const PostArgs post{p->d_lp, p->jac, p->renorm};
@@ -138,7 +138,7 @@ static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long
     const long long H = count;
     if (fused) {
         const SampleArgs sa{p->n_free, nullptr, nullptr, nullptr, nullptr, p->d_run, s, half, pd, j0, hfull, pre,
-                            nullptr};
+                            nullptr, 0, pre_next};
         h->sample_fused[p->ext](st, h->epochs(), h->n, h->n_inst, nullptr, H, h->p_full(), post, sa);
         return;
     }
@@ -155,10 +155,17 @@ static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long
     }
 }
 
+#ifndef RVK_PREFETCH_DRAWS
+#define RVK_PREFETCH_DRAWS 1   // each fused half-step touches the next half-step's draw row (L2-resident when read)
+#endif
 // Kernels of n steps (both halves, all proposals) reading the block's RunArgs and draw table.
 static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
     for (int s = 0; s < n; ++s)
-        for (int half = 0; half < 2; ++half) enqueue_half(p, st, s, half, 0, H, H, p->tab.block);
+        for (int half = 0; half < 2; ++half) {
+            // the next half-step's draws, within this block's n steps (never past the table)
+            const PreDraw *next = (half == 0 || s + 1 < n) ? p->tab.block + ((long long)s * 2 + half + 1) * H : nullptr;
+            enqueue_half(p, st, s, half, 0, H, H, p->tab.block, RVK_PREFETCH_DRAWS ? next : nullptr);
+        }
 }
 
 // A whole block of steps (2 x draws_block_steps(H) half-step kernels) as one HIP graph, captured

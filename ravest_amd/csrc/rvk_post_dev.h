@@ -416,6 +416,7 @@ struct SampleArgs {
     const PreDraw *pre;         // [steps][2][hfull] the draws, indexed by (step, half, j0 + w)
     double *out;                // SAMPLE == 3: out[w] = the proposal's log-posterior (no accept / reject)
     long long qstride;          // SAMPLE & 16 (DIRECT): row stride of q, the given free coordinates
+    const PreDraw *pre_next;    // the next half-step's draw row [hfull] (prefetched into L2), or nullptr
 };
 
 // Limits of the fused proposal path (loglike_kernel SAMPLE >= 2): lane c of the walker's wave
