@@ -156,7 +156,7 @@ static void enqueue_half(rvk_post *p, hipStream_t st, int s, int half, long long
 }
 
 #ifndef RVK_PREFETCH_DRAWS
-#define RVK_PREFETCH_DRAWS 1   // each fused half-step touches the next half-step's draw row (L2-resident when read)
+#define RVK_PREFETCH_DRAWS 0   // 1: each fused half-step touches the next half-step's draw row into L2 (measured +-0)
 #endif
 // Kernels of n steps (both halves, all proposals) reading the block's RunArgs and draw table.
 static void enqueue_steps(rvk_post *p, hipStream_t st, long long H, int n) {
