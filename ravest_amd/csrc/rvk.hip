@@ -183,7 +183,9 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     // registers first and stored to LDS only after the walker's draw / row loads are issued, so
     // the prologue is three memory round trips (constants and draws || rows || barrier), not a
     // chain of a wait per kind of load
-    constexpr bool TDEF = FUSE && RVK_FUSE_PROLOGUE && RVK_TAB_LDS && BLK >= kTabN;
+    // (the plain likelihood likewise when its prep reads the global table: the LDS copy is
+    // stored after the prep's row loads and conversion, before the pass barrier)
+    constexpr bool TDEF = RVK_FUSE_PROLOGUE && RVK_TAB_LDS && BLK >= kTabN && (FUSE || !TP || RVK_PREP_GTAB);
 #if RVK_TAB_LDS
     __shared__ SC tab[kTabN];
     double tab_s = 0.0, tab_c = 0.0;   // (scalars: a struct here is promoted to a per-thread LDS copy)
@@ -343,6 +345,11 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             pks[j][p] = pk;
             okp[j][p] = ok;
         }
+#if RVK_TAB_LDS
+        if constexpr (TDEF) {
+            if (base == (long long)blockIdx.x * wb && threadIdx.x < kTabN) tab[threadIdx.x] = SC{tab_s, tab_c};
+        }
+#endif
         LL_MARK(2);
         __syncthreads();
         }
