@@ -11,7 +11,7 @@ rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "^FAILED|Error" $O/
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python bench.py --steps 20 --warmup 5 > $O/bench_under_rocprof.json 2> $O/rocprof.err || { tail -20 $O/rocprof.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 20 --warmup 5 > $O/bench_under_rocprof.json 2> $O/rocprof.err || { tail -20 $O/rocprof.err; exit 1; }
 find $O/prof -type f ! -name "*stats*" -delete
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29561 --log-dir $O/tr_logs --redirects 3 --tee 3 bench.py --group --steps 20 --warmup 5 --no-cpu-baseline --no-gp --no-predictive --no-host-path > $O/bench_group.out 2> $O/bench_group.err || { tail -30 $O/bench_group.err; exit 1; }
 python - "$O" <<'PY'
