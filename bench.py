@@ -741,7 +741,9 @@ def main():
     eager_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))   # includes event/launch overhead
 
     # PCIe-inclusive host-buffer path (rvk_loglike: H2D theta, kernel, D2H), for DESIGN.md only
-    host_ms = _med_us(lambda: eng.loglike(theta), 200) * 1e-3     # median of 200 blocking calls
+    # median of 200 blocking calls (skipped with --no-host-path: these zero-copy launches of the same
+    # kernel read theta over PCIe, so they would mix into a profile's per-kernel average)
+    host_ms = None if args.no_host_path else _med_us(lambda: eng.loglike(theta), 200) * 1e-3
 
     # ---- the timed steps -------------------------------------------------------------------
     # graph (default): G-step HIP graphs replayed (S independent streams per graph); eager: K
