@@ -53,6 +53,9 @@ namespace {
 #ifndef RVK_FUSE_PROLOGUE
 #define RVK_FUSE_PROLOGUE 1           // fused kernel prologue: loads first, LDS stores after (see loglike_kernel)
 #endif
+#ifndef RVK_FUSE_SLOTREG
+#define RVK_FUSE_SLOTREG 1            // fused prep: the lane's prior slot copied to registers before the prior formula
+#endif
 #ifndef RVK_FUSE_COMPOSE
 #define RVK_FUSE_COMPOSE 0            // fused prep: operands straight from q by the composed column map (1): measured 18.4 vs 17.9 us per step, off
 #endif
@@ -371,6 +374,15 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 const int D = pd.n_free;
                 const Fetch f = (base == (long long)blockIdx.x * wb && j == wv) ? pre : fetch(w);
                 lp_old_s = f.lpo;                         // (needed only in the epilogue)
+                // this lane's prior slot (kind, source column, constants) read from LDS into registers
+                // up front: the kind's formula then waits on no LDS read of its own
+                PriorSlot ps_r{};
+                if (RVK_FUSE_SLOTREG && lane < pd.n_prior) {
+                    ps_r.kind = fsl[lane].kind;
+                    ps_r.src = fsl[lane].src;
+#pragma unroll
+                    for (int i = 0; i < RVK_PRIOR_NPAR; ++i) ps_r.p[i] = fsl[lane].p[i];
+                }
                 const double q_s = lane < D ? (DIRECT ? f.a : stretch_q(f.b, f.a, f.z)) : 0.0;
                 if (ACCEPT && lane < D) {                 // parked for the epilogue (read back by the same lane)
                     fq[j][lane] = q_s;
@@ -405,7 +417,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     for (int k = 0; k < 5; ++k) p5[k] = col(5 * pl + k);
                     // the prior-side conversion (Case 3, fit.py:3418-3446): lane p < NP converts
                     // planet p; a ValueError rejects the walker; a slot with src < 0 reads it
-                    const int src = lane < pd.n_prior ? fsl[lane].src : 0;
+                    const int src = lane < pd.n_prior ? (RVK_FUSE_SLOTREG ? ps_r.src : fsl[lane].src) : 0;
                     double xv = col(src < 0 ? 0 : src);
                     if constexpr (EXT) {
                         double d5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -418,9 +430,11 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                                 if (src < 0 && dj == k) xv = v;
                             }
                         }
-                        if (lane < pd.n_prior) term = prior_lp(fsl[lane], xv);
+                        if (lane < pd.n_prior) term = RVK_FUSE_SLOTREG ? prior_lp(ps_r, xv) : prior_lp(fsl[lane], xv);
                     } else {
-                        if (lane < pd.n_prior) term = prior_lp_basic(fsl[lane].kind, fsl[lane].p, xv);
+                        if (lane < pd.n_prior)
+                            term = RVK_FUSE_SLOTREG ? prior_lp_basic(ps_r.kind, ps_r.p, xv)
+                                                    : prior_lp_basic(fsl[lane].kind, fsl[lane].p, xv);
                     }
                     if (lane < NP) {
                         PlanetK pk;
