@@ -474,8 +474,8 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             } else {
                 for (int p = 0; p < np; ++p) all_ok &= okp[j][p] != 0;
             }
-            // the loop's constants are read before the validity test (every address is valid either
-            // way): their loads overlap the okp read instead of waiting behind it
+            double res = -INFINITY;
+            if (all_ok && lpw != -INFINITY) {
             const double *g = row + 5 * np;
             const double *jit = g + n_inst;
             const double gd = jit[n_inst], gdd = jit[n_inst + 1];
@@ -483,8 +483,6 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             PlanetK pk[NP > 0 ? NP : 1];
 #pragma unroll
             for (int p = 0; p < NP; ++p) pk[p] = NP >= RVK_PK_SGPR ? uniform_pk(pks[j][p]) : pks[j][p];
-            double res = -INFINITY;
-            if (all_ok && lpw != -INFINITY) {
             double chi2 = 0.0, prod = 0.5;   // prod * 2^expo = running product of s^2
             int expo = 1;
             // The epoch loop, versioned on the (wave-uniform) trend so the trend-free
