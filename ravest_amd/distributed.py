@@ -191,9 +191,13 @@ class ShardedDeviceSampler(_DevicePipeline):
     one fused kernel per half-step instead of evaluate + update.)
 
     ``keep_chain``: "all", or the rank that stores the chain (in its HBM with the default
-    ``chain_storage``, or its host memory with "host"; the others keep only the device chunk);
-    ``get_autocorr_time`` is computed on that rank (rank 0 for "all") and broadcast, so call it
-    on every rank, as ravest's convergence loop does.  A ``GPLogPosterior`` (GPFitter.run_mcmc,
+    ``chain_storage``, or its host memory with "host"; the others keep only the device chunk).
+    Every rank counts the steps and acceptances alike (``iteration``, ``naccepted``), keeping a
+    chain or not.  With one keeping rank ``get_autocorr_time`` is computed there and broadcast (a
+    collective: call it on every rank, as ravest's convergence loop does); with "all" every rank
+    holds the same chain and computes it locally (no collective; the chain storage is decided
+    collectively at each ``sample`` call, so every rank's estimate takes the same code path and
+    the ranks' convergence decisions agree).  A ``GPLogPosterior`` (GPFitter.run_mcmc,
     fit.py:4983-4990) shards the same way over rvk_gp_stretch_draws / _propose / _update; its
     chain equals DeviceEnsembleSampler(GPLogPosterior)'s bit for bit."""
 
@@ -325,16 +329,28 @@ class ShardedDeviceSampler(_DevicePipeline):
             raise RuntimeError(f"rank {self.rank} keeps no chain (keep_chain={self.keep_chain})")
         return super().get_log_prob(flat=flat, thin=thin, discard=discard)
 
-    def get_autocorr_time(self, discard=0, thin=1, **kwargs):
-        """emcee's estimate, computed on ONE rank (keep_chain, or rank 0 with keep_chain="all") and
-        broadcast (collective: call it on every rank, as ravest's convergence loop does).  Every
-        rank then holds the same tau, so a convergence test cannot break on one rank and not on
-        another (with chain_storage="auto" one rank may keep its chain on the host and another in
-        HBM, whose FFTs round differently)."""
+    def _device_chain_fits(self, iterations: int) -> bool:
+        """chain_storage="auto": the device chain grows only if it fits on EVERY rank (one MIN
+        all-reduce; sample() is collective already), so all ranks keep their chains in the same
+        storage and their autocorrelation estimates round alike."""
+        fits = super()._device_chain_fits(iterations)
+        if not self.grouped or self.chain_storage_requested != "auto" or self.keep_chain != "all":
+            return fits
         import torch
-        if not self.grouped:
+        f = torch.tensor([1 if fits else 0], dtype=torch.int32, device=self.device if self.rccl else "cpu")
+        self.dist.all_reduce(f, op=self.dist.ReduceOp.MIN, group=self.group)
+        return bool(int(f[0]))
+
+    def get_autocorr_time(self, discard=0, thin=1, **kwargs):
+        """emcee's estimate.  keep_chain="all": computed locally on each rank (every rank holds the
+        same chain bits in the same storage, so the estimates are equal; no collective).  One
+        keeping rank: computed there and broadcast (collective: call it on every rank, as
+        ravest's convergence loop does), so a convergence test cannot break on one rank and not
+        on another."""
+        import torch
+        if not self.grouped or self.keep_chain == "all":
             return super().get_autocorr_time(discard=discard, thin=thin, **kwargs)
-        src = 0 if self.keep_chain == "all" else self.keep_chain
+        src = self.keep_chain
         tau = torch.zeros(self.ndim, dtype=torch.float64, device=self.device if self.rccl else "cpu")
         err = torch.zeros(1, dtype=torch.float64, device=tau.device)
         if self.rank == src:

@@ -657,7 +657,8 @@ class _DevicePipeline(_SamplerBase):
 
     def _enqueue(self, n: int, dev_store: bool = False, store: bool = True) -> _Chunk:
         """Launch the next n steps.  dev_store: into the device backend's rows (no copy-out);
-        store: the steps are saved (backend rows, acceptance counts)."""
+        store: emcee's flag -- the steps count (iteration, acceptance counts; backend rows on the
+        ranks that keep the chain)."""
         import torch
         stream = self._stream()
         slot = self._nslot % 2
@@ -746,11 +747,15 @@ class _DevicePipeline(_SamplerBase):
             if rstate0 is not None and getattr(self, "rng", None) == "emcee":
                 self.random.set_state(rstate0)
             self._set_state(st)
-        store = store and self._keep_host
-        if store and self._dev_chain and not self._device_chain_fits(iterations):
+        # store (emcee's flag) decides what COUNTS -- iteration and the acceptance counts advance on
+        # every rank alike, so ravest's convergence loop (fit.py:1123-1131) runs the same collective
+        # calls everywhere; keep decides whether this process also writes the chain rows
+        # (keep_chain of the sharded sampler: the other ranks count steps but hold no rows).
+        keep = store and self._keep_host
+        if keep and self._dev_chain and not self._device_chain_fits(iterations):
             self._chain_to_host()
-        dev_store = store and self._dev_chain
-        if store:
+        dev_store = keep and self._dev_chain
+        if keep:
             self.backend.grow(iterations)
         bar = _progress_bar(progress, iterations)
         done, pending = 0, None
@@ -771,7 +776,7 @@ class _DevicePipeline(_SamplerBase):
                     raise ValueError("Probability function returned NaN")
                 b = self.backend
                 a, e = pending.row0, (pending.row0 or 0) + pending.n     # backend rows (store only)
-                if store and not dev_store:   # multi-threaded copy out of the pinned staging
+                if keep and not dev_store:    # multi-threaded copy out of the pinned staging
                     _copy(b.chain[a:e], sc[:pending.n])
                     _copy(b.log_prob[a:e], sl[:pending.n])
                 if self._trace is not None:
@@ -785,7 +790,7 @@ class _DevicePipeline(_SamplerBase):
                     if bar is not None:
                         bar.update(pending.n)
                     yield (_DeviceState(b.chain[e - 1], b.log_prob[e - 1]) if dev_store else
-                           State(b.chain[e - 1], log_prob=b.log_prob[e - 1]) if store else
+                           State(b.chain[e - 1], log_prob=b.log_prob[e - 1]) if keep else
                            State(sc[pending.n - 1].numpy(), log_prob=sl[pending.n - 1].numpy(), copy=True)
                            if sc is not None else State(np.empty((0, self.ndim))))
                     if nxt is None:
@@ -802,7 +807,7 @@ class _DevicePipeline(_SamplerBase):
                         b.iteration = t + 1
                     if dev_store:
                         state = _DeviceState(b.chain[t], b.log_prob[t])
-                    elif store:
+                    elif keep:
                         state = State(b.chain[t], log_prob=b.log_prob[t])
                     elif sc is not None:
                         state = State(sc[i].numpy(), log_prob=sl[i].numpy(), copy=True)

@@ -14,6 +14,7 @@ import torch
 import torch.multiprocessing as mp
 
 W, D, STEPS, SPC = 48, 3, 23, 5
+LOOP_STEPS = 400
 
 
 def _free_port():
@@ -52,6 +53,17 @@ def _worker(rank, world, port, q, mode, storage="auto"):
                 q.put((rank, "no error"))
             except ValueError as e:
                 q.put((rank, str(e), s.iteration))
+        elif mode == "keeploop":                           # ravest's adaptive loop, chain on rank 0 only
+            from tests.test_sampler import ravest_convergence_loop
+            s = _sampler(keep=0, storage=storage)
+            hist = ravest_convergence_loop(s, _x0(), LOOP_STEPS, 25, 50)
+            q.put((rank, s.iteration, s.naccepted.copy(), sorted(hist), s.acceptance_fraction.copy()))
+        elif mode == "tau_all":                            # keep_chain="all": no collective in the estimate
+            s = _sampler(storage=storage)
+            s.run_mcmc(_x0(), 60)
+            tau = s.get_autocorr_time(tol=0) if rank == 1 else None   # one rank only: must not block
+            dist.barrier()
+            q.put((rank, tau, s.get_autocorr_time(tol=0)))
         elif mode == "keep":
             s = _sampler(keep=0, storage=storage)
             s.run_mcmc(_x0(), STEPS)
@@ -148,3 +160,28 @@ def test_device_chain_moves_to_host_when_it_no_longer_fits():
     assert np.array_equal(s.get_chain(), ref.get_chain())
     assert np.array_equal(s.get_log_prob(), ref.get_log_prob())
     assert np.array_equal(s.naccepted, ref.naccepted)
+
+
+@pytest.mark.parametrize("storage", ["host", "device"])
+def test_convergence_loop_with_chain_on_one_rank(storage):
+    """keep_chain=0: the ranks that keep no chain still count iteration and acceptances, so
+    ravest's convergence loop (fit.py:1123-1131) makes the same collective get_autocorr_time
+    calls on every rank and stops at the same step (before: those ranks never left
+    iteration 0 and every rank blocked in the broadcast)."""
+    res = _spawn(2, "keeploop", storage)
+    ref = _sampler()
+    from tests.test_sampler import ravest_convergence_loop
+    hist = ravest_convergence_loop(ref, _x0(), LOOP_STEPS, 25, 50)
+    for rank, it, nacc, checks, af in res:
+        assert it == ref.iteration and it > 0, rank
+        assert np.array_equal(nacc, ref.naccepted), rank
+        assert checks == sorted(hist), rank
+        assert np.all(np.isfinite(af)) and np.array_equal(af, ref.acceptance_fraction), rank
+
+
+def test_autocorr_time_local_with_keep_chain_all():
+    """keep_chain="all": get_autocorr_time is computed locally (a call on one rank alone does not
+    block), and every rank's estimate is the same."""
+    res = _spawn(2, "tau_all")
+    assert res[0][1] is None and res[1][1] is not None
+    assert np.array_equal(res[0][2], res[1][2]) and np.array_equal(res[1][1], res[1][2])
