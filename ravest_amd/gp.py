@@ -33,7 +33,7 @@ import numpy as np
 
 from . import _lib
 from .param import Parameterisation, as_parameterisation, full_param_names
-from .prior import _BUILTIN, as_priors, device_params, logpdf_vec
+from .prior import as_priors, is_builtin, device_params, logpdf_vec
 
 SUPPORTED_KERNELS = ["Quasiperiodic"]
 HYPERPARAMS = ["gp_amp", "gp_lambda_e", "gp_lambda_p", "gp_period"]   # gp.py:37, the C-ABI hyper row order
@@ -263,8 +263,8 @@ class GPLogPosterior:
         """Where the priors and hyperpriors are evaluated: "device" (DeviceGPPosterior, one host
         round trip) when every one is a built-in prior class, else "host"."""
         if self._route == "auto":
-            ok = all(isinstance(self._pp._priors[k], _BUILTIN) for k in self._pp._prior_order) and \
-                all(isinstance(self._hyperpriors[k], _BUILTIN) for k in self.free_hyperparams_names)
+            ok = all(is_builtin(self._pp._priors[k]) for k in self._pp._prior_order) and \
+                all(is_builtin(self._hyperpriors[k]) for k in self.free_hyperparams_names)
             self._route = "device" if ok else "host"
         return self._route
 

@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _lib
 from .param import Parameterisation, as_parameterisation, full_param_names
-from .prior import _BUILTIN, Uniform, as_priors, device_params, logpdf_vec
+from .prior import Uniform, is_builtin, as_priors, device_params, logpdf_vec
 
 
 class LogLikelihood:
@@ -232,7 +232,7 @@ class LogPosterior:
         if self._route == "auto":
             from .engine import RVEngine
             eng = self.log_likelihood._engine
-            ok = all(isinstance(self._priors[k], _BUILTIN) for k in self._prior_order) and \
+            ok = all(is_builtin(self._priors[k]) for k in self._prior_order) and \
                 (eng is None or isinstance(eng, RVEngine))
             self._route = "device" if ok else "host"
         return self._route

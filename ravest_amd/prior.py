@@ -254,8 +254,10 @@ def as_prior(prior):
     prior's public attributes (ravest.prior.Uniform(lower, upper), ...) becomes the
     equivalent built-in here (same validation, same formulas); anything else is a custom
     callable and stays one (host path, evaluated per walker like the reference)."""
-    if isinstance(prior, _BUILTIN):
+    if is_builtin(prior):
         return prior
+    if isinstance(prior, _BUILTIN):   # a user subclass of a built-in: its overrides are honoured
+        return prior                  # (host path, per-walker __call__), never the parent's formula
     name = type(prior).__name__
     attrs = PUBLIC_ATTRS.get(name)
     if attrs is not None and all(hasattr(prior, a) for a in attrs):
@@ -271,13 +273,19 @@ def as_priors(priors: dict) -> dict:
 def logpdf_vec(prior, x) -> np.ndarray:
     """Vectorised log-prior for any prior: built-ins use ``logpdf``; user callables are
     evaluated per element (the reference's per-walker semantics)."""
-    if hasattr(prior, "logpdf"):
+    if is_builtin(prior):
         return prior.logpdf(x)
     x = _arr(x)
     return np.array([float(prior(float(v))) for v in x.ravel()]).reshape(x.shape)
 
 
 _BUILTIN = (Uniform, EccentricityUniform, Normal, TruncatedNormal, HalfNormal, Rayleigh, VanEylen19Mixture, Beta)
+
+
+def is_builtin(prior) -> bool:
+    """Exactly one of the built-in classes (a subclass may override __call__ / logpdf, so it is
+    a custom callable: host path, its own formula)."""
+    return type(prior) in _BUILTIN
 
 
 # ---- device form (include/rvk_post.h RVK_PRIOR_*) --------------------------------------------
@@ -298,6 +306,9 @@ def device_params(prior):
     prior = as_prior(prior)
     p = np.zeros(_lib.PRIOR_NPAR)
     name = type(prior).__name__
+    if not is_builtin(prior):
+        raise NotImplementedError(f"prior {prior!r} ({name}) is not one of the built-in classes (a subclass "
+                                  f"keeps its own formula on the host path); built-in priors: {PRIOR_FUNCTIONS}")
     if isinstance(prior, Uniform):
         p[:3] = prior.lower, prior.upper, -np.log(prior.upper - prior.lower)
     elif isinstance(prior, EccentricityUniform):

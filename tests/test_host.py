@@ -155,3 +155,37 @@ def test_log_probability_dict_of_arrays_is_vectorised():
     assert got.shape == (len(x),)
     assert np.array_equal(got, lpost.log_probability_batch(x), equal_nan=True)
     assert lpost.log_probability({n: float(v[0]) for n, v in d.items()}) == got[0] or np.isnan(got[0])
+
+
+def test_prior_subclass_keeps_its_own_formula():
+    """A user subclass of a built-in prior that overrides __call__ is a custom callable: the
+    routed drop-in keeps the host-prior path (its formula), and it has no device form."""
+    class HalfUniform(P.Uniform):
+        def __call__(self, value):
+            return super().__call__(value) - np.log(2.0)
+
+    case = load_case("cfg2")
+    m = case["meta"]
+    k0 = next(iter(m["priors"]))
+    lpost = _posterior(case)
+    lpost.log_likelihood._engine, lpost._route = None, "auto"     # as with the real engine
+    assert lpost.route == "device"
+    c, kw = m["priors"][k0]
+    sub = HalfUniform(**kw) if c == "Uniform" else None
+    if sub is None:
+        pytest.skip("the first prior of the case is not a Uniform")
+    assert P.as_prior(sub) is sub and not P.is_builtin(sub)
+    with pytest.raises(NotImplementedError):
+        P.device_params(sub)
+    np.testing.assert_array_equal(P.logpdf_vec(sub, np.array([0.5 * (kw["lower"] + kw["upper"])])),
+                                  [P.Uniform(**kw)(0.5 * (kw["lower"] + kw["upper"])) - np.log(2.0)])
+    priors = {k: (sub if k == k0 else getattr(P, cc)(**kk)) for k, (cc, kk) in m["priors"].items()}
+    lp2 = LogPosterior(m["planet_letters"], Parameterisation(m["parameterisation"]), priors, m["fixed"],
+                       m["free_names"], case["time"], case["vel"], case["velerr"], case["instrument"],
+                       np.array(m["unique_instruments"]), m["t0"], engine=_ZeroEngine())
+    host = _posterior(case).log_probability_batch(case["theta_free"])
+    sub_lp = lp2.log_probability_batch(case["theta_free"])
+    fin = np.isfinite(host)
+    np.testing.assert_allclose(sub_lp[fin], host[fin] - np.log(2.0), rtol=0, atol=1e-9)
+    lp2.log_likelihood._engine, lp2._route = None, "auto"
+    assert lp2.route == "host"
