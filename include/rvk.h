@@ -26,6 +26,18 @@
  *   P_full = 5*n_planets + 2*n_inst + 2 (a larger row stride is allowed).
  * Instrument index i refers to ravest's np.unique (sorted) instrument order
  * (fit.py:113, 3585-3586).
+ *
+ * Threading.  The blocking host-buffer entry points (rvk_loglike, rvk_predict,
+ * rvk_logpost, rvk_gp_loglike, rvk_gp_predict, rvk_gp_logpost) may be called from
+ * several threads on one handle, or on posteriors / GP objects built on one handle:
+ * they share the handle's stream and host staging, so a per-handle mutex serialises
+ * them (ravest hands log_probability to emcee's map or pool, fit.py:1068-1075; a
+ * thread pool works, calls on one handle just take turns -- create one handle per
+ * thread for concurrency).  The stream-ordered *_device entry points, the samplers'
+ * rvk_*stretch* calls, rvk_*reserve and rvk_set_option are NOT serialised: each
+ * object's device workspace is single-owner, so order such calls on one object
+ * yourself (one thread, or one stream with the caller's own lock).  rvk_destroy
+ * must not race any call on the handle or the objects built on it.
  */
 #ifndef RVK_H
 #define RVK_H
@@ -134,6 +146,13 @@ int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, 
 #define RVK_HOSTIO_PAGEABLE  1
 #define RVK_HOSTIO_PINNED    2
 #define RVK_HOSTIO_ZEROCOPY  3
+/* RVK_OPT_LDS_POISON (tests only; default 0): every kernel that stages the sin/cos table in
+ * LDS first writes each entry as NaN and the real value ~10 us later, before the barrier
+ * that publishes the table.  A read of the table that is not ordered after that barrier
+ * then sees NaN and the results are NaN: the GPU parity tests run with it on to catch a
+ * publish-order race (round 4 found one that green tests had missed).  Same results when
+ * the kernels are race-free; slower. */
+#define RVK_OPT_LDS_POISON 5
 int rvk_set_option(rvk_handle *h, int32_t key, int32_t value);
 
 /* Stream the handle uses (hipStream_t as void*). */
@@ -144,7 +163,8 @@ int rvk_device_count(void);
 const char *rvk_last_error(void);
 /* 100*major + minor.  101: rvk_stretch_run / rvk_gp_stretch_run take an int32 flags
  * argument after step0 and rvk_stretch_half is gone (a caller built against 100 must
- * not call them); RVK_OPT_HOSTIO added. */
+ * not call them); RVK_OPT_HOSTIO added.  102: RVK_OPT_LDS_POISON; the blocking calls
+ * are serialised per handle (Threading, above). */
 int rvk_version(void);
 
 #ifdef __cplusplus

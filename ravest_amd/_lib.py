@@ -194,6 +194,7 @@ def addr(a) -> int:
 
 HOSTIO = {"auto": 0, "pageable": 1, "pinned": 2, "zerocopy": 3}   # include/rvk.h RVK_HOSTIO_*
 OPT_HOSTIO = 4
+OPT_LDS_POISON = 5
 
 
 def check(rc: int) -> None:

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64 * NW, (MAXR == 2 ? 4 : 2)) void gp_loglike_kerne
         asm volatile("; agpr hint %0" : "+a"(z));
     }
 #endif
-    for (int i = tid; i < kTabN; i += NT) L.tab[i] = d.tab[i];
+    for (int i = tid; i < kTabN; i += NT) tab_put(L.tab, i, d.tab[i], d.poison);
     for (int i = tid; i < nt * nt; i += NT) L.slot[i] = slots[i];
     __syncthreads();   // the table is read by the planet prep below (threads < np), before any other barrier
     float *A = work + (long long)blockIdx.x * work_stride;
@@ -984,6 +984,13 @@ static void free_gp(rvk_gp *g) {
     delete g;
 }
 
+// LDS a workgroup may allocate on this device (gfx950: 160 KB; the runtime reports it as the
+// per-CU or the per-block figure, whichever it fills in).
+static size_t lds_per_cu(const hipDeviceProp_t &prop) {
+    const size_t a = prop.maxSharedMemoryPerMultiProcessor, b = prop.sharedMemPerBlock;
+    return a > b ? a : b;
+}
+
 // The fp32 factorisation's launch shape and workspace (n <= kGpF32MaxEpochs: its column panel
 // lives in LDS).
 static int create_gp32(rvk_gp *g, rvk_handle *h, const hipDeviceProp_t &prop) {
@@ -996,7 +1003,7 @@ static int create_gp32(rvk_gp *g, rvk_handle *h, const hipDeviceProp_t &prop) {
     if (!g->launch) return fail(RVK_E_ARG, "GP supports 1..32 planets");
     g->lds = gp_lds_bytes(h->n, h->n_planets, sh.nw);
     // workgroups that fit at once (LDS-limited), each with its own workspace
-    const size_t per_cu = (size_t)160 * 1024 / g->lds;
+    const size_t per_cu = lds_per_cu(prop) / g->lds;
     g->grid = (unsigned)(prop.multiProcessorCount * (per_cu < 1 ? 1 : (per_cu > (size_t)wgpcu ? (size_t)wgpcu : per_cu)));
     const int nt = (h->n + TB - 1) / TB;
     std::vector<short> slots;
@@ -1025,8 +1032,10 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     g->cond64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, true, s64);
     if (!g->launch64 || !g->cond64) return fail(RVK_E_ARG, "GP supports 1..32 planets");
     g->lds64 = gp64_lds_bytes(h->n, h->n_planets, s64.nw);
-    if (g->lds64 > (size_t)160 * 1024) return fail(RVK_E_ARG, "GP fp64 kernel: LDS need exceeds 160 KB");
-    g->grid64 = (unsigned)prop.multiProcessorCount;
+    if (g->lds64 > lds_per_cu(prop))
+        return fail(RVK_E_ARG, "GP fp64 kernel: LDS need (" + std::to_string(g->lds64) + " B) exceeds the device's " +
+                                   std::to_string(lds_per_cu(prop)) + " B per workgroup");
+    g->grid64 = (unsigned)prop.multiProcessorCount * (unsigned)(8 / s64.nw);   // 8 waves per CU
     g->w64stride = gp64_work_doubles(h->n);
     HIPCHK(hipMalloc(&g->d_work64, sizeof(double) * (size_t)g->w64stride * g->grid64));
     return RVK_OK;
@@ -1123,6 +1132,7 @@ int rvk_gp_loglike(rvk_gp *g, const double *theta, const double *hyper, int64_t 
     if (!theta || !hyper || !out || W < 0) return fail(RVK_E_ARG, "bad host buffers");
     rvk_handle *h = g->h;
     if (stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad walker block shape");
+    std::lock_guard<std::mutex> lock(h->mu);   // one blocking call per handle at a time (rvk.h, threading)
     HIPCHK(hipSetDevice(h->device));
     const size_t b[2] = {sizeof(double) * (size_t)W * (size_t)stride, sizeof(double) * (size_t)W * (size_t)hstride};
     const size_t bo = sizeof(double) * (size_t)W;
@@ -1163,6 +1173,7 @@ int rvk_gp_predict(rvk_gp *g, const double *theta, const double *hyper, int64_t 
     if (!theta || !hyper || !tq || !out || S < 0 || T < 0) return fail(RVK_E_ARG, "bad host buffers");
     rvk_handle *h = g->h;
     if (stride < h->p_full() || hstride < RVK_GP_NHYPER) return fail(RVK_E_ARG, "bad sample block shape");
+    std::lock_guard<std::mutex> lock(h->mu);   // one blocking call per handle at a time (rvk.h, threading)
     HIPCHK(hipSetDevice(h->device));
     const size_t bt = sizeof(double) * (size_t)S * (size_t)stride, bh = sizeof(double) * (size_t)S * (size_t)hstride;
     const size_t bq = sizeof(double) * (size_t)T, bo = sizeof(double) * (size_t)S * (size_t)T;
@@ -1364,6 +1375,7 @@ int rvk_gp_logpost(rvk_gp_post *p, const double *xf, int64_t W, int64_t stride, 
     if (W == 0) return RVK_OK;
     if (!xf || !out) return fail(RVK_E_ARG, "NULL host buffer");
     rvk_handle *h = p->g->h;
+    std::lock_guard<std::mutex> lock(h->mu);   // one blocking call per handle at a time (rvk.h, threading)
     HIPCHK(hipSetDevice(h->device));
     const size_t bx = sizeof(double) * (size_t)W * (size_t)stride, bo = sizeof(double) * (size_t)W;
     const void *src = xf, *d_x = nullptr;

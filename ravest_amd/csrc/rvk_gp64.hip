@@ -457,7 +457,7 @@ constexpr bool gp64_ldsp() { return RVK_GP64_LDSPARK && MAXR == 3 && !GROUPED; }
 // MAXR tile rows per row-owning wave; GROUPED: nt > MAXR * (NW - 1), the rows go through the workspace in
 // groups of MAXR (a separate instantiation: the common shape keeps its register allocation)
 template <int NW, int MAXR, bool COND, bool GROUPED>
-__global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a) {
     constexpr int NT = 64 * NW;
     extern __shared__ double smem64[];
     const int n = a.n, ni = a.ni, np = a.np;
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     const int wr = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave owns tile rows wr, wr + NW, ...
     const EpochData &d = a.d;
     const bool multi = ni > 1, tp = d.par == RVK_PAR_PKEWTP;
-    for (int i = tid; i < kTabN; i += NT) tab[i] = d.tab[i];
+    for (int i = tid; i < kTabN; i += NT) tab_put(tab, i, d.tab[i], d.poison);
     __syncthreads();   // the table is read by the planet prep below (threads < np), before any other barrier
     double *wk = a.work + (long long)blockIdx.x * a.work_stride;
 
@@ -995,8 +995,12 @@ void launch_gp64(hipStream_t st, unsigned grid, size_t lds, const Gp64Args &a) {
 
 namespace rvk {
 
+#ifndef RVK_GP64_NW4
+#define RVK_GP64_NW4 0   // experiment: 4-wave workgroups, two per CU (two walkers' step chains interleave on a CU)
+#endif
 Gp64Shape gp64_shape(int n) {
     const int nt = (n + TB - 1) / TB;
+    if (RVK_GP64_NW4) return Gp64Shape{4, 3, true};
     // 7 row-owning waves + the factor wave; beyond 7 x 5 tile rows the rows are grouped
     return nt <= 16 ? Gp64Shape{8, 3, false} : nt <= 35 ? Gp64Shape{8, 5, false} : Gp64Shape{8, 5, true};
 }
@@ -1004,7 +1008,8 @@ Gp64Shape gp64_shape(int n) {
 size_t gp64_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * ((RVK_GP64_SINADD ? 4 : 3) * (size_t)nt * TB + TB * FS + TILE + 2 * (size_t)nw);
-    if (gp64_shape(n).maxr == 3 && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
+    const Gp64Shape sh = gp64_shape(n);
+    if (sh.maxr == 3 && !sh.grouped && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
     return b;
 }
@@ -1018,6 +1023,9 @@ gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape s
     (void)multi;
     (void)tp;
     if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
+#if RVK_GP64_NW4
+    if (sh.nw == 4) return condition ? launch_gp64<4, 3, true, true> : launch_gp64<4, 3, false, true>;
+#endif
     if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true, false> : launch_gp64<8, 3, false, false>;
     if (!sh.grouped) return condition ? launch_gp64<8, 5, true, false> : launch_gp64<8, 5, false, false>;
     return condition ? launch_gp64<8, 5, true, true> : launch_gp64<8, 5, false, true>;

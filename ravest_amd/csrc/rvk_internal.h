@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 
 #include "../../include/rvk.h"
@@ -28,7 +29,21 @@ struct EpochData {
     int par;              // parameterisation code (RVK_PAR_*)
     int lpw;              // lanes per walker: 0 = chosen per launch, else 64 / 32 / 16 (RVK_OPT_LPW)
     int np;               // planets (the generic kernels' runtime count; the others are specialised)
+    int poison;           // RVK_OPT_LDS_POISON: tab_put writes NaN first (tests only)
 };
+
+// Store entry i of an LDS copy of the sin/cos table.  poison (RVK_OPT_LDS_POISON, tests only):
+// NaN first, the real value ~10 us later (the compiler barrier keeps the first store), so a
+// reader not ordered after the publishing barrier sees NaN.
+__device__ __forceinline__ void tab_put(SC *tab, int i, SC v, int poison) {
+    if (poison) {
+        tab[i] = SC{__builtin_nan(""), __builtin_nan("")};
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        for (int k = 0; k < 3; ++k) __builtin_amdgcn_s_sleep(127);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    tab[i] = v;
+}
 
 // Optional log-posterior epilogue of the log-likelihood kernel (fit.py:3461-3495):
 // lp == nullptr: out = log-likelihood.  Otherwise lp[w] is the walker's log-prior
@@ -151,8 +166,12 @@ struct rvk_handle {
     int graph = 0;                           // RVK_OPT_GRAPH
     int lpw = 0;                             // RVK_OPT_LPW
     int hostio = RVK_HOSTIO_AUTO;            // RVK_OPT_HOSTIO, shared by the posteriors built on the handle
+    int poison = 0;                          // RVK_OPT_LDS_POISON
     rvk::HostIO io;                          // rvk_loglike's transport
+    // Held by every blocking (host-buffer) entry point of this handle and of the posteriors /
+    // GP objects built on it: they share the handle's stream and staging (include/rvk.h).
+    std::mutex mu;
 
-    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw, n_planets}; }
+    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw, n_planets, poison}; }
     int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }
 };

@@ -413,6 +413,7 @@ int rvk_logpost(rvk_post *p, const double *xf, int64_t W, int64_t stride, double
     if (W == 0) return RVK_OK;
     if (!xf || !out) return fail(RVK_E_ARG, "NULL host buffer");
     rvk_handle *h = p->h;
+    std::lock_guard<std::mutex> lock(h->mu);   // one blocking call per handle at a time (rvk.h, threading)
     HIPCHK(hipSetDevice(h->device));
     int rc = reserve_impl(p, W);       // before staging: a failed allocation leaves nothing in flight
     if (rc) return rc;

@@ -324,7 +324,11 @@ class DevicePosterior:
     (fit.py:3426-3444 dict order) with each prior's constants, and the two
     correction constants.  ``__call__`` (host arrays) and ``device`` (torch
     tensors, stream-ordered) then run the jitter check, the prior-side conversion,
-    the priors, the log-likelihood and the corrections in two kernels.  Only the
+    the priors, the log-likelihood and the corrections in ONE kernel (the likelihood
+    kernel's DIRECT mode: each wave builds its walker's row, checks and priors, then runs
+    its epoch loop) when the posterior fits the fused limits (<= 64 free parameters, full
+    columns and priors; <= 4 planets), else in two (the log-prior kernel, then the
+    likelihood with the posterior epilogue; same bits).  Only the
     built-in priors have a device form; a custom callable prior raises
     NotImplementedError (use ``LogPosterior.log_probability_batch``)."""
 

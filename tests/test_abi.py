@@ -33,7 +33,7 @@ def test_version_and_errors_without_gpu():
     import torch
     from ravest_amd import _lib
     L = _lib.load()
-    assert L.rvk_version() == 101          # 101: stretch-run flags argument, RVK_OPT_HOSTIO
+    assert L.rvk_version() == 102          # 102: RVK_OPT_LDS_POISON, blocking calls serialised per handle
     if torch.cuda.is_available():
         pytest.skip("this checks the no-device error path")
     t = np.linspace(0, 10, 8)

@@ -154,3 +154,45 @@ def test_one_kernel_logpost_equals_two_kernel_path(name, monkeypatch):
     two = _posterior(case).device_posterior()(x)
     assert np.array_equal(one, two, equal_nan=True)
     assert_ll_close(one, case["log_prob"], what=f"one-kernel-{name}")
+
+
+def test_threads_share_one_posterior():
+    """Two Python threads drive the routed drop-in of ONE posterior (and the engine under it) at
+    once, as a thread-pool log_prob_fn would (fit.py:1068-1075; ctypes releases the GIL in the
+    call): the handle's mutex serialises the blocking calls that share its stream and staging,
+    so every result equals the single-threaded one bit for bit (include/rvk.h, Threading)."""
+    import threading
+    case = load_case("cfg2")
+    lpost = _posterior(case)
+    assert lpost.route == "device"
+    x = case["theta_free"]
+    halves = (x[: len(x) // 2], x[len(x) // 2:])
+    ref_b = [lpost.log_probability_batch(h) for h in halves]
+    names = case["meta"]["free_names"]
+    ref_d = [lpost.log_probability(dict(zip(names, h[0]))) for h in halves]
+    eng = lpost.log_likelihood.engine
+    full = lpost._full(x)
+    ref_e = eng.loglike(full) if full is not None else None
+    errors = []
+
+    def work(k):
+        try:
+            for it in range(150):
+                b = lpost.log_probability_batch(halves[k])
+                if not np.array_equal(b, ref_b[k], equal_nan=True):
+                    errors.append((k, it, "batch"))
+                d = lpost.log_probability(dict(zip(names, halves[k][0])))
+                if not (d == ref_d[k] or (np.isnan(d) and np.isnan(ref_d[k]))):
+                    errors.append((k, it, "dict"))
+                if ref_e is not None and it % 10 == 0 and not np.array_equal(eng.loglike(full), ref_e, equal_nan=True):
+                    errors.append((k, it, "engine"))
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts), "a thread hung"
+    assert not errors, errors[:5]

@@ -1,0 +1,86 @@
+"""The LDS publish-order guard (RVK_OPT_LDS_POISON, include/rvk.h): with the option on, every
+kernel that stages the sin/cos table in LDS writes each entry as NaN first and the real value
+~10 us later, before the barrier that publishes it.  A table read that is not ordered after that
+barrier (the race round 4 found in every table-filling kernel, which green parity tests had
+missed) then reads NaN and turns the walker's result NaN -- so these tests fail if a read moves
+ahead of its barrier again.  With the kernels race-free the poisoned run gives the same bits as
+the normal one, which is what they check, on config 2 (the headline kernel), config 3 (the
+segmented kernel), a shard of config 4 (2 planets), the device log-posterior and fused sampler
+kernels, the posterior predictive and config 5's GP shape (fp64 and fp32 factorisations)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(ds):
+    from ravest_amd.engine import RVEngine
+    return RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, len(ds.unique_instruments), len(ds.planet_letters),
+                    ds.parameterisation, ds.t0, device=0)
+
+
+def _both(eng, fn):
+    eng.set_lds_poison(False)
+    a = fn()
+    eng.set_lds_poison(True)
+    try:
+        b = fn()
+    finally:
+        eng.set_lds_poison(False)
+    return a, b
+
+
+@pytest.mark.parametrize("cfg,W", [(2, None), (3, 16384), (4, 8192)])
+def test_loglike_poisoned_table_same_bits(cfg, W):
+    from ravest_amd.synth import make_config
+    ds = make_config(cfg, n_walkers=W)
+    eng = _engine(ds)
+    a, b = _both(eng, lambda: eng.loglike(ds.theta))
+    assert np.isfinite(a).sum() > 0.9 * len(a)
+    assert np.array_equal(a, b, equal_nan=True), f"config {cfg}: {np.isnan(b).sum()} NaN walkers with the poisoned table"
+    # the device-resident form too (the launch the bench times)
+    th = torch.from_numpy(ds.theta).cuda()
+    out = torch.empty(len(ds.theta), dtype=torch.float64, device="cuda")
+
+    def dev():
+        eng.loglike_device(th, out)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+    a2, b2 = _both(eng, dev)
+    assert np.array_equal(a2, a, equal_nan=True) and np.array_equal(b2, a, equal_nan=True)
+
+
+def test_posterior_sampler_predictive_poisoned_table_same_bits():
+    from ravest_amd.sampler import DeviceEnsembleSampler
+    from ravest_amd.synth import make_posterior
+    lpost, x0 = make_posterior(2, n_walkers=1024, device=0)
+    eng = lpost.log_likelihood.engine
+    dp = lpost.device_posterior()
+    a, b = _both(eng, lambda: dp(x0))
+    assert np.array_equal(a, b, equal_nan=True), "device log-posterior (DIRECT kernel)"
+
+    def run():
+        s = DeviceEnsembleSampler(lpost, 1024, seed=3)
+        s.run_mcmc(x0, 16)
+        return np.concatenate([s.get_chain().ravel(), s.get_log_prob().ravel()])
+    a, b = _both(eng, run)
+    assert np.array_equal(a, b, equal_nan=True), "fused stretch-move half-step"
+    from ravest_amd.synth import make_config
+    ds = make_config(2, n_walkers=512)
+    e2 = _engine(ds)
+    tq = np.linspace(ds.time.min(), ds.time.max(), 300)
+    a, b = _both(e2, lambda: e2.predict(ds.theta, tq))
+    assert np.array_equal(a, b, equal_nan=True), "posterior predictive"
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32+fp64"])
+def test_gp_poisoned_table_same_bits(precision):
+    from ravest_amd.gp import GPKernel, GPLogLikelihood
+    from ravest_amd.synth import make_gp_config
+    ds, th, hy = make_gp_config(n_walkers=256)
+    gp = GPLogLikelihood(ds.time, ds.vel, ds.velerr, ds.t0, ds.instrument, ds.unique_instruments, ds.planet_letters,
+                         ds.parameterisation, GPKernel("Quasiperiodic"), precision=precision)
+    a, b = _both(gp.engine, lambda: gp.batch(th, hy))
+    assert np.isfinite(a).sum() > 0.9 * len(a)
+    assert np.array_equal(a, b, equal_nan=True), f"GP {precision}: {np.isnan(b).sum()} NaN walkers when poisoned"

@@ -68,7 +68,7 @@ def test_sharded_gp_sampler_one_rank_equals_single_gpu():
     assert sh.exchange_bytes_per_half_step == (W // 2) * 8
 
 
-def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2, gp=False):
+def _run_ranks(tmp_path, backend, port, W=256, steps=40, nproc=2, gp=False):
     out = tmp_path / f"chain_{backend}_{nproc}{'_gp' if gp else ''}.npz"
     env = dict(os.environ, RVK_TEST_BACKEND=backend, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -84,7 +84,11 @@ def _run_ranks(tmp_path, backend, port, W=256, steps=10, nproc=2, gp=False):
     assert np.array_equal(got["nacc"], ref.naccepted)
     assert int(got["xbytes"]) == (W // 2) * 8
     assert got["nacc"].sum() > 0
-    assert np.array_equal(got["tau"], ref.get_autocorr_time(tol=0), equal_nan=True)   # short chains: NaN tau
+    tau_ref = ref.get_autocorr_time(tol=0)
+    # long enough that every walker has moved: a finite estimate for every parameter, so the
+    # broadcast from the chain's rank is checked on real values, not on NaN == NaN
+    assert np.all(np.isfinite(tau_ref)), tau_ref
+    assert np.array_equal(got["tau"], tau_ref)
     for tag in ("even", "padded"):
         if f"post_{tag}" in got.files:
             assert np.array_equal(got[f"post_{tag}"], got[f"post_{tag}_ref"]), tag
@@ -98,11 +102,11 @@ def test_sharded_sampler_two_ranks_gloo(tmp_path):
 def test_sharded_gp_sampler_two_ranks_gloo(tmp_path):
     """GPFitter.run_mcmc's sampler over two ranks (gloo, both on cuda:0): each rank evaluates half of
     every half-step's GP proposals; the chain equals the single-GPU GP sampler's bit for bit."""
-    _run_ranks(tmp_path, "gloo", 29536, W=32, steps=6, gp=True)
+    _run_ranks(tmp_path, "gloo", 29536, W=32, steps=60, gp=True)
 
 
 def test_rccl_world_one_gp(tmp_path):
-    _run_ranks(tmp_path, "nccl", 29537, W=32, steps=6, nproc=1, gp=True)
+    _run_ranks(tmp_path, "nccl", 29537, W=32, steps=60, nproc=1, gp=True)
 
 
 def test_rccl_world_one(tmp_path):

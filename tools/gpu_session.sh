@@ -8,10 +8,10 @@
 #   bench      the driver's command: bench.py --steps 20 --warmup 5
 #   prof       the same command under rocprofv3 --kernel-trace --stats (stats kept)
 #   profnh     bench.py --no-host-path under rocprofv3 (the device-resident launches only)
-#   kbench     tools/kbench.py: the in-tree library, then every varlib/librvk_*.so, interleaved (REPS)
+#   kbench     tools/kbench.py: the in-tree library, then every $VARDIR/librvk_*.so (default varlib/), interleaved (REPS)
 #   decomp     tools/decomp.py (trivial / 1-epoch / N, W sweeps) on the in-tree library
 #   lltrace    tools/ll_trace.py on varlib/trace/librvk_lltrace.so (tools/ll_trace.sh builds it)
-#   sampler    tools/sampler_bench.py: in-tree library, then every varlib/librvk_*.so, interleaved
+#   sampler    tools/sampler_variants.py (raw device stretch move, 3 posteriors + config 3): in-tree, then variants
 #   gp64       tools/gp_bench.py 4096 512 fp64: in-tree library, then varlib/librvk_*.so
 #   gp32       tools/gp_bench.py 4096 512 fp32: in-tree library, then varlib/librvk_*.so
 #   group      bench.py --group on a world-size-1 RCCL group
@@ -22,7 +22,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 REPS=${REPS:-3}
-VARS=$(ls varlib/librvk_*.so 2>/dev/null)
+VARS=$(ls ${VARDIR:-varlib}/librvk_*.so 2>/dev/null)
 fail() { echo "FAILED: $1"; tail -30 "$2" 2>/dev/null; exit 1; }
 ab() {   # ab NAME TIMEOUT cmd...: in-tree library then each variant, REPS interleaved rounds
   local name=$1 to=$2; shift 2
@@ -64,7 +64,7 @@ for step in "$@"; do
       > $O/bench_under_rocprof_nh.json 2> $O/rocprof_nh.err || fail profnh $O/rocprof_nh.err
     find $O/profnh -type f ! -name "*stats*" -delete; echo "profnh: done" ;;
   kbench)  ab kbench 200 python tools/kbench.py ;;
-  sampler) ab sampler 200 python tools/sampler_bench.py ;;
+  sampler) ab sampler 300 python tools/sampler_variants.py uniform beta vaneylen cfg3 ;;
   gp64)    ab gp64 150 python tools/gp_bench.py 4096 512 fp64 ;;
   gp32)    ab gp32 150 python tools/gp_bench.py 4096 512 fp32 ;;
   decomp)

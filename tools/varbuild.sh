@@ -1,12 +1,13 @@
 #!/bin/bash
 # Build A/B variants of librvk.so into varlib/ (travels to the GPU box; git-ignored):
-#   TUS="rvk" tools/varbuild.sh name1:"-DFOO=1 -DBAR=2" name2:"..."  -> varlib/librvk_<name>.so
+#   TUS="rvk" VAROUT=varlib/x tools/varbuild.sh name1:"-DFOO=1" name2:"..."  -> $VAROUT/librvk_<name>.so
 # The translation units in TUS (default: all four) are rebuilt with the flags (objects under
 # build/var/<name>/); the others are linked from the in-tree build (build/obj, make first).
 # Variants build in parallel.
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p varlib
+OUT=${VAROUT:-varlib}
+mkdir -p $OUT
 ALL="rvk rvk_post rvk_gp rvk_gp64"
 TUS=${TUS:-$ALL}
 one() {
@@ -22,9 +23,9 @@ one() {
     fi
   done
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o varlib/librvk_$name.so $objs
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/librvk_$name.so $objs
   cat $o/*.res > $o/resource.txt 2>/dev/null || true
-  echo "built varlib/librvk_$name.so"
+  echo "built $OUT/librvk_$name.so"
 }
 for spec in "$@"; do
   one "${spec%%:*}" "${spec#*:}" &
