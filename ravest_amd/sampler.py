@@ -438,8 +438,8 @@ class _SamplerBase:
     @staticmethod
     def _unsupported(thin_by, thin, blobs0) -> None:
         if thin is not None or thin_by != 1:
-            raise NotImplementedError("thinned storage (thin_by / thin) is not supported; thin at read time "
-                                      "with get_chain(thin=...)")
+            raise NotImplementedError("the device samplers store every step (thinned storage, thin_by / thin, "
+                                      "is the host EnsembleSampler's); thin at read time with get_chain(thin=...)")
         if blobs0 is not None:
             raise NotImplementedError("blobs are not supported (ravest's log-probabilities have none)")
 
@@ -482,7 +482,25 @@ class EnsembleSampler(_SamplerBase):
 
     def sample(self, initial_state=None, log_prob0=None, rstate0=None, blobs0=None, iterations=1, tune=False,
                skip_initial_state_check=False, thin_by=1, thin=None, store=True, progress=False, progress_kwargs=None):
-        self._unsupported(thin_by, thin, blobs0)
+        """emcee 3.1's EnsembleSampler.sample, including its thinning: ``thin_by=k`` runs k steps per
+        yielded step and stores every k-th; the deprecated ``thin=k`` runs ``iterations`` steps,
+        yields each and stores every k-th (iterations // k rows).  As in emcee, only the stored
+        steps' acceptances are counted (backend.save_step)."""
+        if blobs0 is not None:
+            raise NotImplementedError("blobs are not supported (ravest's log-probabilities have none)")
+        if thin is not None:
+            import warnings
+            warnings.warn("The 'thin' argument is deprecated. Use 'thin_by' instead.", DeprecationWarning)
+            thin = int(thin)
+            if thin <= 0:
+                raise ValueError("Invalid thinning argument")
+            yield_step, checkpoint, nsaves = 1, thin, int(iterations) // thin
+        else:
+            thin_by = int(thin_by)
+            if thin_by <= 0:
+                raise ValueError("Invalid thinning argument")
+            yield_step, checkpoint, nsaves = thin_by, thin_by, int(iterations)
+        iterations = int(iterations)
         st = self._initial(initial_state, log_prob0, skip_initial_state_check)
         if rstate0 is not None:
             self.random.set_state(rstate0)
@@ -491,13 +509,13 @@ class EnsembleSampler(_SamplerBase):
                else np.array(st.log_prob, dtype=np.float64, copy=True))
         self._check_initial_log_prob(lnp)
         if store:
-            self.backend.grow(iterations)
-        bar = _progress_bar(progress, iterations)
+            self.backend.grow(nsaves)
+        bar = _progress_bar(progress, iterations * yield_step)
         a, nd1, b = self.a, self.ndim - 1.0, self.backend
         # emcee keeps ONE State, updates its coordinates and log-probabilities in place and yields
         # it every step (EnsembleSampler.sample); so do we (no per-step copies of the ensemble)
         state = State(x, log_prob=lnp)
-        for _ in range(iterations):
+        for i in range(iterations * yield_step):
             sets, zu, rint, au = emcee_step_draws(self.random, self.nwalkers)
             accepted = np.zeros(self.nwalkers, dtype=bool)
             for split in (0, 1):                               # np.take / np.compress: the same
@@ -515,7 +533,7 @@ class EnsembleSampler(_SamplerBase):
                 x[Sa] = np.compress(acc, q, axis=0)
                 lnp[Sa] = np.compress(acc, new)
                 accepted[Sa] = True
-            if store:                                          # emcee's backend.save_step
+            if store and (i + 1) % checkpoint == 0:           # emcee's backend.save_step
                 b.chain[b.iteration] = x
                 b.log_prob[b.iteration] = lnp
                 b.accepted += accepted
@@ -524,7 +542,8 @@ class EnsembleSampler(_SamplerBase):
             self._previous_state = state
             if bar is not None:
                 bar.update(1)
-            yield state
+            if (i + 1) % yield_step == 0:
+                yield state
         if bar is not None:
             bar.close()
 

@@ -173,3 +173,37 @@ def test_host_sampler_store_false_semantics():
     c = EnsembleSampler(16, 3, f, seed=7)
     c.run_mcmc(x0, 20)
     assert np.array_equal(a.naccepted, b.naccepted - c.naccepted)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_host_sampler_thin_by_stores_every_kth_step(k):
+    """emcee 3.1's thin_by: k steps per yielded step, every k-th stored, and (as in emcee's
+    backend.save_step) only the stored steps' acceptances counted.  Same RandomState stream as an
+    unthinned run, so the stored rows are that run's rows k-1, 2k-1, ..."""
+    f = lambda x: -0.5 * np.sum(x ** 2, axis=1)          # noqa: E731
+    x0 = np.random.default_rng(4).normal(size=(16, 3))
+    ref = EnsembleSampler(16, 3, f, seed=9)
+    acc = []
+    for _ in ref.sample(x0, iterations=12 * k):
+        acc.append(ref.backend.accepted.copy())
+    s = EnsembleSampler(16, 3, f, seed=9)
+    n_yield = sum(1 for _ in s.sample(x0, iterations=12, thin_by=k))
+    assert n_yield == 12 and s.iteration == 12
+    assert np.array_equal(s.get_chain(), ref.get_chain()[k - 1::k])
+    assert np.array_equal(s.get_log_prob(), ref.get_log_prob()[k - 1::k])
+    per_step = np.diff(np.concatenate([np.zeros((1, 16)), np.array(acc)]), axis=0)
+    assert np.array_equal(s.naccepted, per_step[k - 1::k].sum(axis=0))
+
+
+def test_host_sampler_deprecated_thin():
+    f = lambda x: -0.5 * np.sum(x ** 2, axis=1)          # noqa: E731
+    x0 = np.random.default_rng(5).normal(size=(16, 3))
+    ref = EnsembleSampler(16, 3, f, seed=2)
+    ref.run_mcmc(x0, 10)
+    s = EnsembleSampler(16, 3, f, seed=2)
+    with pytest.warns(DeprecationWarning):
+        n_yield = sum(1 for _ in s.sample(x0, iterations=10, thin=3))
+    assert n_yield == 10 and s.iteration == 3                # iterations // thin rows
+    assert np.array_equal(s.get_chain(), ref.get_chain()[2::3][:3])
+    with pytest.raises(ValueError):
+        next(s.sample(x0, iterations=3, thin_by=0))

@@ -9,6 +9,7 @@
 #   prof       the same command under rocprofv3 --kernel-trace --stats (stats kept)
 #   profnh     bench.py --no-host-path under rocprofv3 (the device-resident launches only)
 #   kbench     tools/kbench.py: the in-tree library, then every $VARDIR/librvk_*.so (default varlib/), interleaved (REPS)
+#   hostphase  tools/host_phase_probe.py 4096 (the blocking rvk_loglike call by phase): in-tree, then variants
 #   decomp     tools/decomp.py (trivial / 1-epoch / N, W sweeps) on the in-tree library
 #   lltrace    tools/ll_trace.py on varlib/trace/librvk_lltrace.so (tools/ll_trace.sh builds it)
 #   sampler    tools/sampler_variants.py (raw device stretch move, 3 posteriors + config 3): in-tree, then variants
@@ -64,6 +65,7 @@ for step in "$@"; do
       > $O/bench_under_rocprof_nh.json 2> $O/rocprof_nh.err || fail profnh $O/rocprof_nh.err
     find $O/profnh -type f ! -name "*stats*" -delete; echo "profnh: done" ;;
   kbench)  ab kbench 200 python tools/kbench.py ;;
+  hostphase) ab hostphase 150 python tools/host_phase_probe.py 4096 ;;
   sampler) ab sampler 300 python tools/sampler_variants.py uniform beta vaneylen cfg3 ;;
   gp64)    ab gp64 150 python tools/gp_bench.py 4096 512 fp64 ;;
   gp32)    ab gp32 150 python tools/gp_bench.py 4096 512 fp32 ;;
