@@ -59,9 +59,6 @@ namespace {
 #ifndef RVK_FUSE_COMPOSE
 #define RVK_FUSE_COMPOSE 0            // fused prep: operands straight from q by the composed column map (1): measured 18.4 vs 17.9 us per step, off
 #endif
-#ifndef RVK_FUSE_NOBAR
-#define RVK_FUSE_NOBAR 0              // fused half-step with no block barrier: per-wave table copies, lane constants in registers
-#endif
 #ifndef RVK_PREP_GTAB
 #define RVK_PREP_GTAB 1               // prep's sin/cos(w) from the global (L2) table (1), or from the LDS copy behind an
                                       // extra block barrier (0): measured 7.4 vs 7.7 us on config 2
@@ -278,12 +275,6 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     constexpr bool CONV = (SAMPLE & 8) != 0;
     constexpr bool EXT = CONV || (SAMPLE & 4) != 0;
     constexpr int WF = FUSE ? BLK / 64 : 1;   // fused: one walker per wave per pass (launch_sample_fused)
-    // NOBAR (RVK_FUSE_NOBAR): no block barrier at all -- each wave keeps its own LDS copy of the
-    // sin/cos table and its lanes hold the posterior's per-lane constants (column map, fixed
-    // value, prior slot) in registers, so a wave's prep starts when ITS loads arrive instead of
-    // after the block's slowest wave (the loglike_wave_kernel idea applied to the half-step)
-    constexpr bool NOBAR = FUSE && RVK_FUSE_NOBAR;
-    __shared__ SC tabw[NOBAR ? WF : 1][NOBAR ? kTabN : 1];
     __shared__ PlanetK pks[WB][NPA];
     __shared__ int okp[WB][NPA];
     __shared__ double fq[WF][kFuseMaxD], fx[WF][kFuseMaxD], ff[WF][kFuseMaxPFull];
@@ -306,7 +297,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
     // chain of a wait per kind of load
     // (the plain likelihood likewise when its prep reads the global table: the LDS copy is
     // stored after the prep's row loads and conversion, before the pass barrier)
-    constexpr bool TDEF = RVK_FUSE_PROLOGUE && RVK_TAB_LDS && BLK >= kTabN && (FUSE || !TP || RVK_PREP_GTAB) && !NOBAR;
+    constexpr bool TDEF = RVK_FUSE_PROLOGUE && RVK_TAB_LDS && BLK >= kTabN && (FUSE || !TP || RVK_PREP_GTAB);
 #if RVK_TAB_LDS
     __shared__ SC tab[kTabN];
     double tab_s = 0.0, tab_c = 0.0;   // (scalars: a struct here is promoted to a per-thread LDS copy)
@@ -315,34 +306,13 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             tab_s = d.tab[threadIdx.x].s;
             tab_c = d.tab[threadIdx.x].c;
         }
-    } else if constexpr (!NOBAR) {
+    } else {
         for (int i = threadIdx.x; i < kTabN; i += BLK) tab_put(tab, i, d.tab[i], d.poison);
     }
 #else
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
 #endif
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr int TK = (kTabN + 63) / 64;
-    double nts[NOBAR ? TK : 1], ntc[NOBAR ? TK : 1];   // NOBAR: this lane's entries lane + 64 k of the table
-    const SC *tabx;                                     // the LDS table the passes read
-    if constexpr (NOBAR) {
-#pragma unroll
-        for (int k = 0; k < TK; ++k) {
-            nts[k] = ntc[k] = 0.0;
-            if (lane + 64 * k < kTabN) {
-                nts[k] = d.tab[lane + 64 * k].s;
-                ntc[k] = d.tab[lane + 64 * k].c;
-            }
-        }
-        tabx = tabw[wv];
-    } else {
-        tabx = tab;
-    }
-    // NOBAR: the posterior's per-lane constants, lane c: column c's free position or -1 and its
-    // fixed value; lane k: prior slot k (p_full, n_prior <= 64 in the fused kernels)
-    int lc_fc = 0;
-    double lc_tm = 0.0;
-    PriorSlot lc_ps{};
     // FUSE: a wave's proposal draws and reads of the walker rows (emcee's StretchMove), issued
     // for the wave's first walker before the barrier so their latency hides under the table
     // fill; the posterior's constants are staged in LDS (each is read in a loop with a runtime
@@ -404,26 +374,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     reinterpret_cast<const char *>(sa.pre_next + sa.j0 + w0) + zo);   // global_load, not flat
             }
         }
-        if constexpr (NOBAR) {
-            if (lane < sa.pd.p_full) {
-                lc_fc = sa.pd.colmap[lane];
-                lc_tm = sa.pd.tmpl[lane];
-            }
-            if (lane < sa.pd.n_prior) {
-                lc_ps.kind = sa.pd.slots[lane].kind;
-                lc_ps.src = sa.pd.slots[lane].src;
-#pragma unroll
-                for (int i = 0; i < RVK_PRIOR_NPAR; ++i) lc_ps.p[i] = sa.pd.slots[lane].p[i];
-            }
-            if (wv < wb && w0 < n_walkers) pre = fetch(w0);
-            __builtin_amdgcn_sched_barrier(0);   // the table stores wait for the table loads only
-            SC *tw = tabw[wv];
-#pragma unroll
-            for (int k = 0; k < TK; ++k) {
-                if (lane + 64 * k < kTabN) tab_put(tw, lane + 64 * k, SC{nts[k], ntc[k]}, d.poison);
-            }
-            wave_lds_sync();
-        } else if constexpr (RVK_FUSE_PROLOGUE) {
+        if constexpr (RVK_FUSE_PROLOGUE) {
             static_assert(BLK >= kFuseMaxPFull && BLK >= kFuseMaxPrior, "one staging entry per thread");
             const int tid = threadIdx.x;
             const bool stc = tid < sa.pd.p_full, sts = tid < sa.pd.n_prior;
@@ -465,7 +416,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             }
             for (int i = threadIdx.x; i < sa.pd.n_prior; i += BLK) fsl[i] = sa.pd.slots[i];
         }
-        if constexpr (!NOBAR) __syncthreads();   // (also publishes the table)
+        __syncthreads();   // (also publishes the table)
     }
     LL_MARK(0);
     LL_MARK(1);
@@ -536,9 +487,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 // this lane's prior slot (kind, source column, constants) read from LDS into registers
                 // up front: the kind's formula then waits on no LDS read of its own
                 PriorSlot ps_r{};
-                if constexpr (NOBAR) {
-                    ps_r = lc_ps;
-                } else if (RVK_FUSE_SLOTREG && lane < pd.n_prior) {
+                if (RVK_FUSE_SLOTREG && lane < pd.n_prior) {
                     ps_r.kind = fsl[lane].kind;
                     ps_r.src = fsl[lane].src;
 #pragma unroll
@@ -549,10 +498,10 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     fq[j][lane] = q_s;
                     fx[j][lane] = f.a;
                 }
-                const int fc = lane < pd.p_full ? (NOBAR ? lc_fc : fcol[lane]) : 0;
+                const int fc = lane < pd.p_full ? fcol[lane] : 0;
                 double fv = shfl_d(q_s, fc < 0 ? 0 : fc);
                 if (lane < pd.p_full) {
-                    if (fc < 0) fv = NOBAR ? lc_tm : ftm[lane];
+                    if (fc < 0) fv = ftm[lane];
                     ff[j][lane] = fv;
                 }
                 // column c of the full row, per lane: RVK_FUSE_COMPOSE reads it from q through the
@@ -578,7 +527,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                     for (int k = 0; k < 5; ++k) p5[k] = col(5 * pl + k);
                     // the prior-side conversion (Case 3, fit.py:3418-3446): lane p < NP converts
                     // planet p; a ValueError rejects the walker; a slot with src < 0 reads it
-                    const int src = lane < pd.n_prior ? ((RVK_FUSE_SLOTREG || NOBAR) ? ps_r.src : fsl[lane].src) : 0;
+                    const int src = lane < pd.n_prior ? (RVK_FUSE_SLOTREG ? ps_r.src : fsl[lane].src) : 0;
                     double xv = col(src < 0 ? 0 : src);
                     if constexpr (EXT) {
                         double d5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -591,15 +540,15 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                                 if (src < 0 && dj == k) xv = v;
                             }
                         }
-                        if (lane < pd.n_prior) term = (RVK_FUSE_SLOTREG || NOBAR) ? prior_lp(ps_r, xv) : prior_lp(fsl[lane], xv);
+                        if (lane < pd.n_prior) term = RVK_FUSE_SLOTREG ? prior_lp(ps_r, xv) : prior_lp(fsl[lane], xv);
                     } else {
                         if (lane < pd.n_prior)
-                            term = (RVK_FUSE_SLOTREG || NOBAR) ? prior_lp_basic(ps_r.kind, ps_r.p, xv)
+                            term = RVK_FUSE_SLOTREG ? prior_lp_basic(ps_r.kind, ps_r.p, xv)
                                                     : prior_lp_basic(fsl[lane].kind, fsl[lane].p, xv);
                     }
                     if (lane < NP) {
                         PlanetK pk;
-                        const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tabx) : planet_consts(d.par, p5, pk);
+                        const bool ok = TP ? planet_consts_t<0, RVK_PREP_TAB>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
                         pks[j][lane] = pk;
                         okp[j][lane] = ok;
                     }
@@ -642,7 +591,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             PlanetK pk[NP > 0 ? NP : 1];
 #pragma unroll
             for (int p = 0; p < NP; ++p) pk[p] = NP >= RVK_PK_SGPR ? uniform_pk(pks[j][p]) : pks[j][p];
-            const double tot = epoch_sum<NP, MULTI, SOLVER>(d, n_epochs, n_inst, g, jit, pk, pks[j], np, tabx, t_1, v_1,
+            const double tot = epoch_sum<NP, MULTI, SOLVER>(d, n_epochs, n_inst, g, jit, pk, pks[j], np, tab, t_1, v_1,
                                                             s_1, i_1, lane);
             LL_MARK(5);
             res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
@@ -684,105 +633,12 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
                 LL_MARK(6);
             }
         }
-        if (base + (long long)gridDim.x * wb < n_walkers) {   // LDS rows are rewritten next pass
-            if constexpr (NOBAR) wave_lds_sync();             // (fused: every slot is the wave's own)
-            else __syncthreads();
-        }
+        if (base + (long long)gridDim.x * wb < n_walkers) __syncthreads();   // LDS rows are rewritten next pass
     }
     LL_MARK(7);
     if constexpr (FUSE && ACCEPT && !DIRECT) {   // a use of the prefetched word (a no-op if it ever fires)
         asm volatile("" : "+v"(pf_draw));   // the word is consumed here, at the end, not earlier
         if (pf_draw == 0x7fc0dead && lane == 0) atomicOr(sa.run->status, 0);
-    }
-}
-
-// Wave-autonomous variant of the plain likelihood (RVK_LL_WAVE; NP = 1 .. 4, P_full <= 64,
-// production solver): no block barrier anywhere.  Each wave keeps its own LDS copy of the sin/cos
-// table, loads its walker's whole row with ONE lane-parallel load (lane c: column c; one
-// coalesced request -- also over PCIe in the host path's zero-copy transport) and preps its own
-// planets, lanes over planets (lane p < NP converts planet p, as the fused sampler's prep), so a
-// wave's epoch loop starts as soon as ITS row and table copy have arrived instead of after the
-// slowest wave of the block.  The row is parked in the wave's LDS slot for gamma / jit / trend.
-// Issue order at entry: the lane's first epoch, the table, the row -- independent round trips in
-// flight together; the next walker's row is loaded under this walker's epoch loop.  Same
-// arithmetic and order as loglike_kernel (epoch_sum): the results are bitwise the same.
-#ifndef RVK_LL_WAVE
-#define RVK_LL_WAVE 0
-#endif
-#ifndef RVK_LL_WAVE_BLOCK
-#define RVK_LL_WAVE_BLOCK 256
-#endif
-template <int NP, bool MULTI, bool TP, int BLK>
-__global__ __launch_bounds__(BLK, 4 * kBlock / BLK) void loglike_wave_kernel(EpochData d, int n_epochs, int n_inst,
-                                                                            const double *__restrict__ theta,
-                                                                            long long n_walkers, long long stride,
-                                                                            double *__restrict__ out, PostArgs post) {
-    static_assert(NP >= 1 && NP <= 4, "lanes over planets: a handful of planets");
-    constexpr int NW = BLK / 64, TK = (kTabN + 63) / 64;
-    __shared__ SC tabw[NW][kTabN];
-    __shared__ PlanetK pkw[NW][NP];
-    __shared__ double roww[NW][64];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int pf = 5 * NP + 2 * n_inst + 2;   // <= 64 (launch_ll)
-    SC *tab = tabw[wv];
-    double *rw = roww[wv];
-    double t_1 = 0.0, v_1 = 0.0, s_1 = 1.0;
-    int i_1 = 0;
-    if (lane < n_epochs) {
-        t_1 = d.t[lane]; v_1 = d.vel[lane]; s_1 = d.s2[lane];
-        if (MULTI) i_1 = d.inst[lane];
-    }
-    double ts[TK], tc[TK];   // this lane's table entries lane + 64 k (scalars: a struct array goes to scratch)
-#pragma unroll
-    for (int k = 0; k < TK; ++k) {
-        ts[k] = tc[k] = 0.0;
-        if (lane + 64 * k < kTabN) {
-            ts[k] = d.tab[lane + 64 * k].s;
-            tc[k] = d.tab[lane + 64 * k].c;
-        }
-    }
-    const long long wstep = (long long)gridDim.x * NW;
-    long long w = (long long)blockIdx.x * NW + wv;
-    auto load_row = [&](long long ww) { return (ww < n_walkers && lane < pf) ? theta[ww * stride + lane] : 0.0; };
-    double rv = load_row(w);
-    __builtin_amdgcn_sched_barrier(0);   // the stores below wait for the table loads only
-#pragma unroll
-    for (int k = 0; k < TK; ++k) {
-        if (lane + 64 * k < kTabN) tab_put(tab, lane + 64 * k, SC{ts[k], tc[k]}, d.poison);
-    }
-    wave_lds_sync();
-    for (; w < n_walkers; w += wstep) {
-        if (lane < pf) rw[lane] = rv;
-        bool ok = true;
-        {
-            const int pl = lane < NP ? lane : 0;
-            double p5[5];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p5[k] = shfl_d(rv, 5 * pl + k);
-            if (lane < NP) {
-                PlanetK pk;
-                ok = TP ? planet_consts_t<0, true>(p5, pk, 0, tab) : planet_consts(d.par, p5, pk);
-                pkw[wv][lane] = pk;
-            }
-        }
-        const bool all_ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
-        const double lpw = post.lp ? post.lp[w] : 0.0;
-        if (w + wstep < n_walkers) rv = load_row(w + wstep);   // the next walker's row, under this one's loop
-        wave_lds_sync();
-        double res = -INFINITY;
-        if (all_ok && lpw != -INFINITY) {
-            PlanetK pk[NP];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) pk[p] = NP >= RVK_PK_SGPR ? uniform_pk(pkw[wv][p]) : pkw[wv][p];
-            const double *g = rw + 5 * NP;
-            const double tot = epoch_sum<NP, MULTI, 0>(d, n_epochs, n_inst, g, g + n_inst, pk, pkw[wv], NP, tab, t_1,
-                                                       v_1, s_1, i_1, lane);
-            res = -0.5 * (tot + (double)n_epochs * kLog2Pi);
-            if (post.lp) res = ((res + lpw) + post.jac) + post.renorm;   // fit.py:3492-3494
-        }
-        if (lane == 0) out[w] = res;
-        wave_lds_sync();   // pkw / rw are rewritten for the wave's next walker
     }
 }
 
@@ -1093,16 +949,6 @@ void launch_ll(hipStream_t st, EpochData d, int n, int ni, const double *th, lon
         const int lpw = choose_lpw(d.lpw, NP, n, W);
         if (lpw == 32) return launch_seg<NP, MULTI, TP, 32>(st, d, n, ni, th, W, stride, out, post);
         if (lpw == 16) return launch_seg<NP, MULTI, TP, 16>(st, d, n, ni, th, W, stride, out, post);
-    }
-    if constexpr (RVK_LL_WAVE && SOLVER == 0 && NP >= 1 && NP <= 4) {
-        if (5 * NP + 2 * ni + 2 <= 64) {   // the row in one lane-parallel load
-            constexpr int NW = RVK_LL_WAVE_BLOCK / 64;
-            long long blocks = (W + NW - 1) / NW;
-            if (blocks > 65536) blocks = 65536;
-            hipLaunchKernelGGL((loglike_wave_kernel<NP, MULTI, TP, RVK_LL_WAVE_BLOCK>), dim3((unsigned)blocks),
-                               dim3(RVK_LL_WAVE_BLOCK), 0, st, d, n, ni, th, W, stride, out, post);
-            return;
-        }
     }
     long long blocks;
     int wb;

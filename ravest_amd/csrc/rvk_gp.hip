@@ -1035,7 +1035,7 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     if (g->lds64 > lds_per_cu(prop))
         return fail(RVK_E_ARG, "GP fp64 kernel: LDS need (" + std::to_string(g->lds64) + " B) exceeds the device's " +
                                    std::to_string(lds_per_cu(prop)) + " B per workgroup");
-    g->grid64 = (unsigned)prop.multiProcessorCount * (unsigned)(8 / s64.nw);   // 8 waves per CU
+    g->grid64 = (unsigned)prop.multiProcessorCount;
     g->w64stride = gp64_work_doubles(h->n);
     HIPCHK(hipMalloc(&g->d_work64, sizeof(double) * (size_t)g->w64stride * g->grid64));
     return RVK_OK;

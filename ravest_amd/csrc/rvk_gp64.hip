@@ -63,10 +63,6 @@ __device__ unsigned long long g_gp64_trace[8][32][8];
 #define G64_MARK(k, slot) do {} while (0)
 #endif
 
-#ifndef RVK_GP64_FLOW
-#define RVK_GP64_FLOW 0   // the step schedule as dataflow between waves (flag_wait) instead of 3 barriers per step
-#endif
-constexpr int kFlowInts = 64;     // LDS ints for RVK_GP64_FLOW (fdone, dready, bad, s1w[<= 12], s1row[<= 48])
 constexpr int TB = 32;            // tile edge
 constexpr int TILE = TB * TB;     // doubles per tile
 constexpr int FS = 34;            // row stride (doubles) of the factor's row buffer: 16-byte aligned rows
@@ -94,27 +90,6 @@ __device__ __forceinline__ int felem(int row, int col) {
 
 // park / unpark / load_frags take a global or an LDS (address_space(3)) tile pointer.
 using lds_d = __attribute__((address_space(3))) double;
-using lds_i = __attribute__((address_space(3))) int;
-
-// RVK_GP64_FLOW: the step schedule as dataflow between the waves of a workgroup instead of three
-// block barriers per step.  Monotonic LDS counters, release-stored by their one producer wave
-// and acquire-polled by the consumers (workgroup scope: every wave is on this CU, whose L1 the
-// workspace tiles go through): a wait gives up after ~2^22 polls and marks the walker bad (its
-// log-likelihood NaN) rather than hang the CU.
-__device__ __forceinline__ int flag_get(lds_i *f) { return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-__device__ __forceinline__ void flag_put(lds_i *f, int v) {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void flag_wait(lds_i *f, int v, lds_i *bad) {
-    int it = 0;
-    while (flag_get(f) < v) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++it > (1 << 22)) {
-            if ((threadIdx.x & 63) == 0) *bad = 1;
-            break;
-        }
-    }
-}
 using v2d = __attribute__((ext_vector_type(2))) double;     // 16-byte pair, any address space
 using lds_v2d = __attribute__((address_space(3))) v2d;
 __device__ __forceinline__ v2d *d2p(double *p) { return reinterpret_cast<v2d *>(p); }
@@ -285,8 +260,7 @@ struct FactorAcc {
     int pexp;
 };
 __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li, lds_d *Lr, double *xdiag,
-                                                           FactorAcc fa, lds_i *gate = nullptr, int ngate = 0,
-                                                           int need = 0, lds_i *bad = nullptr) {
+                                                           FactorAcc fa) {
     const int lane = threadIdx.x & 63;
     double quad = fa.quad, dpr = fa.dpr;
     int pexp = fa.pexp;
@@ -334,8 +308,6 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
         }
     }
     wave_lds_sync();
-    // RVK_GP64_FLOW: li still holds the previous step's -X until every row wave has read it (S1)
-    for (int u = 0; u < ngate; ++u) flag_wait(gate + u, need, bad);
     if (lane >= 32) {                               // -X, fragment layout
         const int j = lane - 32, kk = j >> 2;
 #pragma unroll
@@ -485,7 +457,7 @@ constexpr bool gp64_ldsp() { return RVK_GP64_LDSPARK && MAXR == 3 && !GROUPED; }
 // MAXR tile rows per row-owning wave; GROUPED: nt > MAXR * (NW - 1), the rows go through the workspace in
 // groups of MAXR (a separate instantiation: the common shape keeps its register allocation)
 template <int NW, int MAXR, bool COND, bool GROUPED>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a) {
+__global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     constexpr int NT = 64 * NW;
     extern __shared__ double smem64[];
     const int n = a.n, ni = a.ni, np = a.np;
@@ -508,13 +480,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
     SC *tab = reinterpret_cast<SC *>(red + 2 * NW);
     PlanetK *pks = reinterpret_cast<PlanetK *>(tab + kTabN);
     int *oks = reinterpret_cast<int *>(pks + np);
-    // RVK_GP64_FLOW's counters (gp64_lds_bytes reserves kFlowInts): steps factored, the step whose
-    // diagonal tile is in fb, the bad-walker mark, per row wave the S1 steps done, per tile row the
-    // S1 steps done
-    constexpr bool FLOW = RVK_GP64_FLOW && LDSP && RVK_GP64_S1HALF && !GROUPED && !COND && RVK_GP64_RING > 1;
-    lds_i *const fl = (lds_i *)(oks + np);
-    lds_i *const f_fdone = fl, *const f_dready = fl + 1, *const f_bad = fl + 2, *const f_s1w = fl + 4,
-                 *const f_s1row = fl + 16;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wr = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave owns tile rows wr, wr + NW, ...
     const EpochData &d = a.d;
@@ -656,7 +621,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
             else if constexpr (LDSP) park(pslot(bi), t, lane);
             else park(wk + tix(bi, 0) * TILE, t, lane);
         };
-        if (FLOW && tid < kFlowInts) fl[tid] = 0;   // (published by the barrier below)
         if (wr < NA) {
             if constexpr (GROUPED) {
                 for (int bi = wr; bi < nt; bi += NA) col0(bi);   // every owned row (also past MAXR)
@@ -671,13 +635,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
             // ---- the factor wave: P(k) for every k, then the step's barriers ----------------------
             for (int k = 0; k < nt; ++k) {
                 G64_MARK(k, 0);
-                if (FLOW && k > 0) flag_wait(f_dready, k, f_bad);   // acc(k, k) in fb (S2(k-1) of row k)
                 __builtin_amdgcn_s_setprio(1);    // the step's critical path goes first on its SIMD
                 if (!(RVK_GP64_ABLATE & 4)) {
-                    // FLOW: -X goes into li once every row wave has read the previous one (S1(k-1))
                     const FactorAcc fa = factor_diag((lds_d *)fb, (lds_d *)li, (lds_d *)(Lr + k * TB),
-                                                     COND ? wk + tix(k, k) * TILE : nullptr, FactorAcc{quad, dpr, pexp},
-                                                     FLOW ? f_s1w : nullptr, FLOW ? NA : 0, k, f_bad);
+                                                     COND ? wk + tix(k, k) * TILE : nullptr, FactorAcc{quad, dpr, pexp});
                     quad = fa.quad;
                     dpr = fa.dpr;
                     pexp = fa.pexp;
@@ -685,10 +646,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
                 __builtin_amdgcn_s_setprio(0);
                 G64_MARK(k, 1);
                 G64_MARK(k, 2);
-                if constexpr (FLOW) {                       // -X and y_k published
-                    flag_put(f_fdone, k + 1);
-                    continue;
-                }
                 __syncthreads();                            // B1: -X and y_k published
                 G64_MARK(k, 3);
                 if (k + 1 == nt) break;
@@ -794,11 +751,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
 #pragma unroll
                         for (int q = MAXR - 1; q >= 0; --q)
                             if (q < nown && rm.bi[q] >= k + 1) r0 = q;
-                        if (k > 0 && r0 < nown && !(RVK_GP64_ABLATE & 8)) {
-                            // FLOW: the A operand row k+1 is another wave's: its L(k+1, j < k) written
-                            if (FLOW) flag_wait(f_s1row + k + 1, k, f_bad);
+                        if (k > 0 && r0 < nown && !(RVK_GP64_ABLATE & 8))
                             accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, rm, lane, r0, nown - 1);
-                        }
                     } else {
                         pass(std::integral_constant<int, 0>{});
                         if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
@@ -814,9 +768,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
                     }
                 }
                 G64_MARK(k, 2);
-                if (FLOW && k + 1 == nt) break;             // (the last step is the factor wave's alone)
-                if constexpr (FLOW) flag_wait(f_fdone, k + 1, f_bad);   // -X and y_k of F(k)
-                else __syncthreads();                       // B1: -X and y_k published
+                __syncthreads();                            // B1: -X and y_k published
                 G64_MARK(k, 3);
                 if (k + 1 == nt) break;
                 // ---- S1(k): L(bi, k) = acc(bi, k) X^T, stored; rhs update ----------------------
@@ -880,7 +832,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
                                 s += __shfl_xor(s, 32);
                                 if (lane < 16) Lr[bi * TB + 16 * qq + lane] -= s;
                             }
-                            if (FLOW) flag_put(f_s1row + bi, k + 1);   // L(bi, k) in T and the slot, r_bi updated
                             continue;
                         }
                         Acc cur;
@@ -923,12 +874,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
                 }
             }
                 G64_MARK(k, 4);
-                if constexpr (FLOW) {
-                    flag_put(f_s1w + wr, k + 1);            // this wave is done with li
-                    flag_wait(f_s1row + k + 1, k + 1, f_bad);   // L(k+1, k) in row k+1's slot
-                } else {
-                    __syncthreads();                        // B2: L(k+1, k) published
-                }
+                __syncthreads();                            // B2: L(k+1, k) published
                 G64_MARK(k, 5);
                 // ---- S2(k): the j = k term; park for S1(k+1), the diagonal tile to fb -----------
             {
@@ -956,10 +902,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
                         const int bi = rm.bi[q];
-                        if (bi > k && bi < nt && q < nown) {
-                            s2(nacc[q], bi);
-                            if (FLOW && bi == k + 1) flag_put(f_dready, k + 1);   // acc(k+1, k+1) in fb
-                        }
+                        if (bi > k && bi < nt && q < nown) s2(nacc[q], bi);
                     }
                 } else {
                     for (int q = 0; q < nown; ++q) {
@@ -972,7 +915,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
                     }
                 }
             }
-                if constexpr (!FLOW) __syncthreads();       // B3: acc(k+1, k+1) in fb
+                __syncthreads();                            // B3: acc(k+1, k+1) in fb
                 G64_MARK(k, 6);
             }
         }
@@ -993,7 +936,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gp64_kernel(const Gp64Args a)
                 }
                 double ll = -0.5 * qs - 0.5 * ls - 0.5 * (double)n * kLog2Pi;
                 if (!__builtin_isfinite(ll)) ll = NAN;             // not positive definite
-                if (FLOW && *f_bad) ll = NAN;                      // a dataflow wait gave up (never expected)
                 if (a.post.lp) ll = (((ll + a.post.lp[w]) + a.post.lhp[w]) + a.post.jac) + a.post.renorm;
                 a.out[w] = ll;
             }
@@ -1053,12 +995,8 @@ void launch_gp64(hipStream_t st, unsigned grid, size_t lds, const Gp64Args &a) {
 
 namespace rvk {
 
-#ifndef RVK_GP64_NW4
-#define RVK_GP64_NW4 0   // experiment: 4-wave workgroups, two per CU (two walkers' step chains interleave on a CU)
-#endif
 Gp64Shape gp64_shape(int n) {
     const int nt = (n + TB - 1) / TB;
-    if (RVK_GP64_NW4) return Gp64Shape{4, 3, true};
     // 7 row-owning waves + the factor wave; beyond 7 x 5 tile rows the rows are grouped
     return nt <= 16 ? Gp64Shape{8, 3, false} : nt <= 35 ? Gp64Shape{8, 5, false} : Gp64Shape{8, 5, true};
 }
@@ -1066,10 +1004,8 @@ Gp64Shape gp64_shape(int n) {
 size_t gp64_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * ((RVK_GP64_SINADD ? 4 : 3) * (size_t)nt * TB + TB * FS + TILE + 2 * (size_t)nw);
-    const Gp64Shape sh = gp64_shape(n);
-    if (sh.maxr == 3 && !sh.grouped && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
+    if (gp64_shape(n).maxr == 3 && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
-    b += sizeof(int) * kFlowInts;   // RVK_GP64_FLOW's counters
     return b;
 }
 
@@ -1082,9 +1018,6 @@ gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape s
     (void)multi;
     (void)tp;
     if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
-#if RVK_GP64_NW4
-    if (sh.nw == 4) return condition ? launch_gp64<4, 3, true, true> : launch_gp64<4, 3, false, true>;
-#endif
     if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true, false> : launch_gp64<8, 3, false, false>;
     if (!sh.grouped) return condition ? launch_gp64<8, 5, true, false> : launch_gp64<8, 5, false, false>;
     return condition ? launch_gp64<8, 5, true, true> : launch_gp64<8, 5, false, true>;
