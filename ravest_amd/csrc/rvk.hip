@@ -90,6 +90,16 @@ __device__ __forceinline__ T ld_off(const T *base, unsigned off) {
     return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
 }
 
+// RVK_OPT_LDS_POISON for the kernels whose first parameter is the EpochData: the flag re-read
+// from the kernel-argument segment where the table is stored (a volatile scalar load, K$-resident),
+// so it holds no SGPR across the prologue (a live flag there cost SGPR spills, ~8 VALU
+// instructions per wave on config 2).
+__device__ __forceinline__ int poison_arg() {
+    using kp = const __attribute__((address_space(4))) char *;
+    const kp p = (kp)__builtin_amdgcn_kernarg_segment_ptr();
+    return *(volatile const __attribute__((address_space(4))) int *)(p + offsetof(EpochData, poison));
+}
+
 // Copy the sin/cos table into LDS (whole block; one barrier, before any
 // per-wave work so no wave can skip it).
 __device__ __forceinline__ void load_tab(SC *lds, const SC *__restrict__ g, int poison = 0) {
@@ -307,7 +317,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             tab_c = d.tab[threadIdx.x].c;
         }
     } else {
-        for (int i = threadIdx.x; i < kTabN; i += BLK) tab_put(tab, i, d.tab[i], d.poison);
+        for (int i = threadIdx.x; i < kTabN; i += BLK) tab_put(tab, i, d.tab[i], poison_arg());
     }
 #else
     const SC *__restrict__ tab = d.tab;   // L1/L2-resident gather, no LDS fill
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
             __builtin_amdgcn_sched_barrier(0);   // the stores below wait for their loads only
 #if RVK_TAB_LDS
             if constexpr (TDEF) {
-                if (tid < kTabN) tab_put(tab, tid, SC{tab_s, tab_c}, d.poison);
+                if (tid < kTabN) tab_put(tab, tid, SC{tab_s, tab_c}, poison_arg());
             }
 #endif
             if (stc) {
@@ -460,7 +470,7 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
 #if RVK_TAB_LDS
         if constexpr (TDEF) {
             if (base == (long long)blockIdx.x * wb && threadIdx.x < kTabN)
-                tab_put(tab, threadIdx.x, SC{tab_s, tab_c}, d.poison);
+                tab_put(tab, threadIdx.x, SC{tab_s, tab_c}, poison_arg());
         }
 #endif
         LL_MARK(2);
@@ -666,7 +676,7 @@ __global__ __launch_bounds__(kBlock, (NP >= 3 ? RVK_SEG_LB3 : 4)) void loglike_s
         t_1 = d.t[li]; v_1 = d.vel[li]; s_1 = d.s2[li];
         if (MULTI) i_1 = d.inst[li];
     }
-    for (int i = threadIdx.x; i < kTabN; i += kBlock) tab_put(tab, i, d.tab[i], d.poison);
+    for (int i = threadIdx.x; i < kTabN; i += kBlock) tab_put(tab, i, d.tab[i], poison_arg());
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (long long base = (long long)blockIdx.x * wb; base < n_walkers; base += (long long)gridDim.x * wb) {
         const int nb = (int)((n_walkers - base) < wb ? (n_walkers - base) : wb);

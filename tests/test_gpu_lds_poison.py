@@ -84,3 +84,28 @@ def test_gp_poisoned_table_same_bits(precision):
     a, b = _both(gp.engine, lambda: gp.batch(th, hy))
     assert np.isfinite(a).sum() > 0.9 * len(a)
     assert np.array_equal(a, b, equal_nan=True), f"GP {precision}: {np.isnan(b).sum()} NaN walkers when poisoned"
+
+
+@pytest.mark.parametrize("cfg,W", [(2, None), (3, 16384)])
+def test_poison_reaches_the_kernel(cfg, W):
+    """Positive control: the poisoned fill really runs (each filling thread sleeps ~10 us between
+    its NaN and its real store), so a poisoned launch is measurably slower -- the equality tests
+    above would pass vacuously if the flag never reached the kernel."""
+    from ravest_amd.synth import make_config
+    ds = make_config(cfg, n_walkers=W)
+    eng = _engine(ds)
+    th = torch.from_numpy(ds.theta).cuda()
+    out = torch.empty(len(ds.theta), dtype=torch.float64, device="cuda")
+
+    def us_per_launch(n=20):
+        eng.loglike_device(th, out)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(n):
+            eng.loglike_device(th, out)
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) * 1e3 / n
+    plain, poisoned = _both(eng, us_per_launch)
+    assert poisoned > plain + 5.0, (plain, poisoned)
