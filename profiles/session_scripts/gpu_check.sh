@@ -1,6 +1,6 @@
 #!/bin/bash
 # Session check on a GPU box: GPU tests, smoke, bench, GP bench, rocprof kernel stats of both.
-# Usage: bash tools/gpu_check.sh TAG
+# Usage: bash profiles/session_scripts/gpu_check.sh TAG
 TAG=${1:-r}
 O=gpurun_out/$TAG
 mkdir -p $O

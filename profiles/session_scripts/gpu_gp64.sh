@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session: GP tests (fp32 + fp64 + posterior + predictive), then config-5 timing per precision
 # and a rocprof kernel-stats pass.  Every GPU step has its own time limit; the first failure ends it.
-# Usage: bash tools/gpu_gp64.sh TAG
+# Usage: bash profiles/session_scripts/gpu_gp64.sh TAG
 TAG=${1:-gp64}
 O=gpurun_out/$TAG
 mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (tools/pmc.sh) for the config-2, config-3 and config-4-shard likelihood launches;
-# summaries land in gpurun_out/pmcN/pmc_configN.json.  Usage: bash tools/gpu_pmc_all.sh
+# summaries land in gpurun_out/pmcN/pmc_configN.json.  Usage: bash profiles/session_scripts/gpu_pmc_all.sh
 set -e
 declare -A KF=([2]="loglike_kernel<1, false, 0, true, 0, 1024>" [3]="loglike_seg_kernel<3, true, true, 32>" [4]="loglike_seg_kernel<2, false, true, 32>")
 for C in 2 3 4; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session (round 2): GPU tests, smoke, bench, lanes-per-walker A/B, rocprof stats.
 # Every GPU step has its own time limit; the first failure ends the script.
-# Usage: bash tools/gpu_r2.sh TAG [quick]
+# Usage: bash profiles/session_scripts/gpu_r2.sh TAG [quick]
 TAG=${1:-r2}
 O=gpurun_out/$TAG
 mkdir -p $O

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 session check on a GPU box: GPU tests, smoke, bench line.  Usage: bash tools/gpu_r3.sh TAG [pytest args]
+# Round-3 session check on a GPU box: GPU tests, smoke, bench line.  Usage: bash profiles/session_scripts/gpu_r3.sh TAG [pytest args]
 TAG=${1:-r3}
 shift
 O=gpurun_out/$TAG

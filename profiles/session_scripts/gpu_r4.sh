@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 session check on a GPU box.  Usage: bash tools/gpu_r4.sh TAG [pytest selection...]
+# Round-4 session check on a GPU box.  Usage: bash profiles/session_scripts/gpu_r4.sh TAG [pytest selection...]
 # Steps (each under its own time limit, stop at the first failure): the GPU tests given (default:
 # all), smoke, the host-path probe, the N>1 bench path on a world-size-1 RCCL group, the bench line.
 TAG=${1:-r4}

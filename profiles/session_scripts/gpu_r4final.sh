@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 closing session: GPU tests, smoke, the driver's bench line, the same command under
 # rocprofv3 --kernel-trace --stats (stats kept, raw traces dropped), and the N>1 path on a
-# world-size-1 RCCL group.  Usage: bash tools/gpu_r4final.sh TAG
+# world-size-1 RCCL group.  Usage: bash profiles/session_scripts/gpu_r4final.sh TAG
 TAG=${1:-r4final}
 O=gpurun_out/$TAG
 mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU-box session: tests, smoke, bench (+ variants), rocprof kernel trace of the bench command.
-# Usage: bash tools/gpu_round.sh TAG
+# Usage: bash profiles/session_scripts/gpu_round.sh TAG
 TAG=${1:-r}
 O=gpurun_out/$TAG
 mkdir -p $O

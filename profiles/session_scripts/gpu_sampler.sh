@@ -1,7 +1,7 @@
 #!/bin/bash
 # Sampler session: device-posterior / sampler GPU tests, then bench.py's device stretch-move line
 # (HIP events) with the fused half-step and the two-kernel path (RVK_SAMPLER_FUSE=0), and a
-# rocprof kernel-stats pass of the sampler bench.  Usage: bash tools/gpu_sampler.sh TAG
+# rocprof kernel-stats pass of the sampler bench.  Usage: bash profiles/session_scripts/gpu_sampler.sh TAG
 O=gpurun_out/${1:-samp}
 mkdir -p $O
 export TMPDIR=/tmp

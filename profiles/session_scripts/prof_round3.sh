@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 evidence for profiles/: kernel-trace stats of the driver's bench command, then the PMC
-# passes (configs 2/3/4, config-5 GP fp32 and fp64, predictive).  usage: tools/prof_round3.sh OUT [part]
+# passes (configs 2/3/4, config-5 GP fp32 and fp64, predictive).  usage: profiles/session_scripts/prof_round3.sh OUT [part]
 O=${1:-gpurun_out/prof3}
 PART=${2:-all}
 mkdir -p $O
