@@ -253,8 +253,19 @@ __device__ __forceinline__ double qp_cov(const QP &h, double tau) {
 
 // The diagonal factor of one step, one wave (its own register allocation: a 32-double row or
 // inverse column per lane never shares the register file with the accumulators).  fb holds
-// acc(k, k) row-major on entry and the rows of L_kk on exit; li gets -X = -L_kk^-1 in
-// fragment layout (and xdiag, if set); r_k = Lr[0..31] is replaced by y_k = X r_k.
+// acc(k, k) row-major on entry (its rows are then reused for the columns of L); li gets
+// -X = -L_kk^-1 in fragment layout (and xdiag, if set); r_k = Lr[0..31] is replaced by y_k = X r_k.
+// Right-looking: lane i < 32 holds row i of the symmetric acc(k, k) and applies every column m
+// of L to it as soon as the column exists (a[i][t] -= L[i][m] L[t][m], t > m; the whole row, so
+// the rows stay symmetric and the update is the same instruction for every lane); lane 32 + j
+// turns column j of the identity into column j of X by the same update (b[t] -= L[t][m] x[m]).
+// Column m reaches the other lanes through one LDS row (broadcast reads), except L[m+1][m],
+// which the next pivot needs first: that one is read from lane m + 1 directly, so the pivot
+// chain is readlane -> rsq -> scale -> readlane -> one FMA with the other 30 - m updates
+// beside it.  Round 5 (sessions r5rlf / r5rlf3 / r5bal, 3 interleaved reps each, config 5
+// fp64): 5.76-5.88 vs 5.90-5.97 ms for the left-looking form (row r of L read back through LDS
+// before every pivot: 17.4 k cycles per factor vs 15.0 k, tools/gp64_trace.py); every column
+// as scalars (v_readlane, no LDS) 18.3 k; the LDS form without its fence 17.0 k.
 struct FactorAcc {
     double quad, dpr;
     int pexp;
@@ -264,9 +275,6 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
     const int lane = threadIdx.x & 63;
     double quad = fa.quad, dpr = fa.dpr;
     int pexp = fa.pexp;
-    // lane i < 32: row i of acc(k, k); lane 32 + j: column j of the identity, turned into
-    // column j of X = L_kk^-1 by the same updates (forward substitution).  Row r of L
-    // (L[r][m], m < r, written by lane r at steps m) is read back as LDS broadcasts.
     double av[TB];
     const int lr = lane < 32 ? lane : 0;
 #pragma unroll
@@ -274,37 +282,33 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
         const double x = fb[lr * FS + m];
         av[m] = lane < 32 ? x : (m == lane - 32 ? 1.0 : 0.0);
     }
-    wave_lds_sync();
+    wave_lds_sync();   // acc(k, k) is in registers: fb's rows now carry the columns of L
 #pragma unroll
-    for (int r = 0; r < TB; ++r) {
-        // row r of L: every read issued before the first use (one wait, not one per element).
-        // LDS operations of one wave complete in order, so this step's reads see the previous
-        // steps' column writes without a fence.
-        double lrow[TB];
-#pragma unroll
-        for (int m = 0; m < r; ++m) lrow[m] = fb[r * FS + m];
-        double v0 = av[r], v1 = 0.0, v2 = 0.0, v3 = 0.0;
-#pragma unroll
-        for (int m = 0; m < r; ++m) {
-            if ((m & 3) == 0) v0 = __builtin_fma(-av[m], lrow[m], v0);
-            else if ((m & 3) == 1) v1 = __builtin_fma(-av[m], lrow[m], v1);
-            else if ((m & 3) == 2) v2 = __builtin_fma(-av[m], lrow[m], v2);
-            else v3 = __builtin_fma(-av[m], lrow[m], v3);
-        }
-        const double v = (v0 + v1) + (v2 + v3);
-        const double piv = readlane_d(v, r);        // L[r][r]^2 (<= 0 / NaN propagate)
-        // 1 / sqrt(piv): v_rsq_f64 and two Newton steps (quadratic: ~1 ulp), no IEEE sqrt + divide
-        // sequence on the step's critical path
-        double y = __builtin_amdgcn_rsq(piv);
+    for (int m = 0; m < TB; ++m) {
+        const double piv = readlane_d(av[m], m);         // a[m][m] after columns < m: L[m][m]^2
+        double y = __builtin_amdgcn_rsq(piv);            // 1 / L[m][m] (two Newton steps: ~1 ulp)
         y = y * __builtin_fma(-0.5 * piv, y * y, 1.5);
         y = y * __builtin_fma(-0.5 * piv, y * y, 1.5);
-        av[r] = lane == r ? piv * y : v * y;
-        if (lane < 32) fb[lane * FS + r] = av[r];   // column r of L
+        const double c = lane == m ? piv * y : av[m] * y;   // L[i][m] (lane i < 32) or x[m] (lane >= 32)
+        av[m] = c;
         dpr *= piv;
-        if ((r & 7) == 7) {
+        if ((m & 7) == 7) {
             int e;
             dpr = __builtin_frexp(dpr, &e);
             pexp += e;
+        }
+        if (m + 1 < TB) {
+            if (lane < 32) fb[m * FS + lane] = c;        // column m of L, as row m of fb
+            av[m + 1] = __builtin_fma(-c, readlane_d(c, m + 1), av[m + 1]);
+            if (m + 2 < TB) {
+                wave_lds_sync();
+#pragma unroll
+                for (int t2 = (m + 2) & ~1; t2 < TB; t2 += 2) {
+                    const v2d v = *d2p(fb + m * FS + t2);    // L[t2][m], L[t2 + 1][m] (broadcast)
+                    if (t2 >= m + 2) av[t2] = __builtin_fma(-c, v.x, av[t2]);
+                    av[t2 + 1] = __builtin_fma(-c, v.y, av[t2 + 1]);
+                }
+            }
         }
     }
     wave_lds_sync();
@@ -399,12 +403,13 @@ __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__res
         hx = hx < NQ ? hx : NQ - 1;                 // wait counts stay exact on every path
         const int j = hx >> 2, part = hx & 3;
         const int off = j * (TILE / 2) + part * 64;  // double2 units: tiles of row bi are contiguous in j
-        o.a[0] = rowa[off];
-        o.a[1] = rowa[off + 256];
+        const int offa = (RVK_GP64_ABLATE & 1) ? part * 64 : off, offb = (RVK_GP64_ABLATE & 2) ? part * 64 : off;
+        o.a[0] = rowa[offa];
+        o.a[1] = rowa[offa + 256];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            o.b[r][0] = rowb[r][off];
-            o.b[r][1] = rowb[r][off + 256];
+            o.b[r][0] = rowb[r][offb];
+            o.b[r][1] = rowb[r][offb + 256];
         }
     };
     auto consume = [&](const Ops64<R> &o) {

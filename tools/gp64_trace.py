@@ -31,8 +31,13 @@ def main():
             x = b[wv, k]
             row.append(f"{x[1]-x[0]:6d}/{x[2]-x[1]:6d}/{x[3]-x[2]:6d}/{x[4]-x[3]:5d}/{x[5]-x[4]:5d}/{x[6]-x[5]:5d}")
         tot = b[:, k, 6].max() - b[:, k, 0].min() if k < 15 else b[:, k, 3].max() - b[:, k, 0].min()
-        print(f"{k:2d} tot {tot:7d} | " + " ".join(row[:3]) + " ... " + row[7])
+        print(f"{k:2d} tot {tot:7d} | " + " ".join(row))
     print("walker total cycles:", b[:, 15, 3].max() - t0)
+    # per wave, summed over steps 0..14: factor/idle, accumulation, B1 wait, S1, B2 wait, S2
+    d = np.diff(b[:, :15, :7], axis=2).sum(axis=1)
+    names = ["factor/idle", "accum", "B1wait", "S1", "B2wait", "S2"]
+    for wv in range(8):
+        print(f"wave {wv}: " + "  ".join(f"{n} {int(v)}" for n, v in zip(names, d[wv])))
 
 
 if __name__ == "__main__":
