@@ -38,6 +38,16 @@ def main():
     names = ["factor/idle", "accum", "B1wait", "S1", "B2wait", "S2"]
     for wv in range(8):
         print(f"wave {wv}: " + "  ".join(f"{n} {int(v)}" for n, v in zip(names, d[wv])))
+    # which SIMD each wave of a workgroup runs on (HW_REG_HW_ID bits 5:4), over all blocks
+    hw = np.zeros((1024, 8), dtype=np.uint32)
+    lib = _lib.load()
+    if hasattr(lib, "rvk_gp64_hwid_dump") and lib.rvk_gp64_hwid_dump(hw.ctypes.data_as(C.c_void_p)) == 0:
+        from collections import Counter
+        simd = (hw[:256] >> 4) & 3
+        pats = Counter(tuple(int(x) for x in r) for r in simd)
+        print("wave -> SIMD patterns over 256 blocks (waves 0..7):")
+        for pat, cnt in pats.most_common(8):
+            print(f"  {pat}: {cnt}")
 
 
 if __name__ == "__main__":
