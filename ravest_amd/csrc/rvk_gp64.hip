@@ -389,10 +389,20 @@ __device__ __forceinline__ RowMap<MAXR> row_map(int wr, int nt) {
     return m;
 }
 
+// HALFDIAG: a diagonal tile's block above the diagonal (rows 0-15, columns 16-31: C/D block
+// c[1][0]) is never formed -- no covariance, no accumulation MFMAs, no S2 MFMAs: the
+// right-looking factor reads only lane i's a[i][j <= i] (values above the diagonal stay above it),
+// so that block is don't-care; it is left 0.  1/4 of every diagonal tile's MFMAs (the diagonal
+// row is the first live row of its owner's first span): config 5 fp64 5.73-5.79 vs 5.79-5.87 ms
+// (sessions r5hd / r5hd2, 3 + 4 interleaved reps, profiles/round5/ab_gp_round5b.json).
+#ifndef RVK_GP64_HALFDIAG
+#define RVK_GP64_HALFDIAG 1
+#endif
 template <int MAXR, int NA, int A, int B, int D>
 __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, const RowMap<MAXR> &rm,
                                            int lane) {
     constexpr int R = B - A + 1;
+    const bool dg = RVK_GP64_HALFDIAG && rm.bi[A] == k + 1;   // wave-uniform
     const int NQ = 4 * k;                           // quarters (j, part), j < k
     const double2 *rowa = reinterpret_cast<const double2 *>(wk + tix(k + 1, 0) * TILE) + lane;
     const double2 *rowb[R];
@@ -420,9 +430,11 @@ __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__res
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
-                    for (int q = 0; q < 2; ++q)
+                    for (int q = 0; q < 2; ++q) {
+                        if (RVK_GP64_HALFDIAG && r == 0 && p == 1 && q == 0 && dg) continue;
                         acc[A + r].c[p][q] = mfma64(cmp ? o.a[p].y : o.a[p].x, cmp ? o.b[r][q].y : o.b[r][q].x,
                                                     acc[A + r].c[p][q]);
+                    }
     };
 #pragma unroll
     for (int d = 0; d < D - 1; ++d) issue(ops[d], d);
@@ -593,6 +605,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
+                        if (RVK_GP64_HALFDIAG && p == 1 && q == 0 && bi == bj) {   // above the diagonal
+                            A.c[p][q][i] = 0.0;
+                            continue;
+                        }
                         const int gj = bj * TB + 16 * p + (lane >> 4) + 4 * i;
                         const double kv = kval(ti, si, ci, gj);
                         const bool in = gi < n && gj < n, dg = gi == gj;
@@ -897,8 +913,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                         for (int p = 0; p < 2; ++p)
 #pragma unroll
-                            for (int qq = 0; qq < 2; ++qq)
+                            for (int qq = 0; qq < 2; ++qq) {
+                                if (RVK_GP64_HALFDIAG && p == 1 && qq == 0 && bi == k + 1) continue;
                                 acc.c[p][qq] = mfma64(af[p][kk], bf[qq][kk], acc.c[p][qq]);
+                            }
                     if (bi == k + 1) put_diag(acc);
                     else if constexpr (LDSP) park(pslot(bi), acc, lane);
                     else park(wk + tix(bi, k + 1) * TILE, acc, lane);
