@@ -398,6 +398,14 @@ __device__ __forceinline__ RowMap<MAXR> row_map(int wr, int nt) {
 #ifndef RVK_GP64_HALFDIAG
 #define RVK_GP64_HALFDIAG 1
 #endif
+// S1TRI: S1's A operand -X = -L_kk^-1 is lower triangular, so its block of rows 0-15 and columns
+// 16-31 is exactly zero (the factor's inverse lanes never leave 0 above the diagonal for a positive
+// definite tile): the 8 MFMAs of each S1 product that only multiply that block are skipped (the
+// sums they would add are +-0: the same bits, checked with tools/gp_dump.py on the log-likelihood
+// and the conditioned mean): config 5 fp64 5.61-5.74 vs 5.73-5.79 ms (session r5s1, 4 interleaved reps).
+#ifndef RVK_GP64_S1TRI
+#define RVK_GP64_S1TRI 1
+#endif
 template <int MAXR, int NA, int A, int B, int D>
 __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, const RowMap<MAXR> &rm,
                                            int lane) {
@@ -836,7 +844,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                                 for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-                                    for (int p = 0; p < 2; ++p) o[p] = mfma64(xa[p][kk], cu[kk >> 2][kk & 3], o[p]);
+                                    for (int p = 0; p < 2; ++p) {
+                                        if (RVK_GP64_S1TRI && p == 0 && kk >= 4) continue;   // X rows 0-15, cols 16-31: 0
+                                        o[p] = mfma64(xa[p][kk], cu[kk >> 2][kk & 3], o[p]);
+                                    }
                                 double s = 0.0;
 #pragma unroll
                                 for (int p = 0; p < 2; ++p) {
@@ -869,8 +880,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                             for (int p = 0; p < 2; ++p)
 #pragma unroll
-                                for (int qq = 0; qq < 2; ++qq)
+                                for (int qq = 0; qq < 2; ++qq) {
+                                    if (RVK_GP64_S1TRI && p == 0 && kk >= 4) continue;   // X rows 0-15, cols 16-31: 0
                                     o.c[p][qq] = mfma64(xa[p][kk], cur.c[kk >> 2][qq][kk & 3], o.c[p][qq]);
+                                }
                         // o.c[p][qq][i] at lane l = L(bi, k)[16 qq + (l & 15)][16 p + (l >> 4) + 4 i]
                         //                         = frag(qq, 4 p + i)[l]
 #pragma unroll
