@@ -1017,10 +1017,12 @@ loglike_launch_t pick_ll_t(int np, bool multi) {
     return multi ? pick_ll_s<true, SOLVER, TP>(np) : pick_ll_s<false, SOLVER, TP>(np);
 }
 
+#if !RVK_TU_SAMPLE   // (this would instantiate every likelihood kernel in rvk_sample.hip's build too)
 loglike_launch_t pick_ll(int np, bool multi, int solver, bool tp) {
     if (solver == 1) return tp ? pick_ll_t<1, true>(np, multi) : pick_ll_t<1, false>(np, multi);
     return tp ? pick_ll_t<0, true>(np, multi) : pick_ll_t<0, false>(np, multi);
 }
+#endif
 
 // MODE 1: propose_kernel + the likelihood with the accept / reject; 2: one fused half-step;
 // 3: fused proposals, log-posterior out (the fused modes: NP <= 4); | 4: every prior kind;
@@ -1055,6 +1057,27 @@ sample_launch_t pick_sample(int np, bool multi, bool tp) {
     if (multi) return tp ? pick_sample_s<true, true, MODE>(np) : pick_sample_s<true, false, MODE>(np);
     return tp ? pick_sample_s<false, true, MODE>(np) : pick_sample_s<false, false, MODE>(np);
 }
+
+#if RVK_TU_SAMPLE
+}  // namespace
+
+// rvk_sample.hip compiles this file a second time with RVK_TU_SAMPLE: only the kernels that make
+// their own stretch-move proposals (MODE 2 / 3, | 4, | 8), under the iterative-ILP machine scheduler
+// (Makefile).  Measured (session r5flags, tools/sampler_variants.py, 3 interleaved reps): the
+// half-steps 1.5 % (uniform priors) to 6.5 % (VanEylen) faster with it, while the plain likelihood
+// kernels lose 1-3.5 % (tools/kbench.py), so they keep the default scheduler in rvk.hip.
+rvk::sample_launch_t rvk::pick_sample_fused(int mode, int np, bool multi, bool tp) {
+    switch (mode) {
+        case 2: return pick_sample<2>(np, multi, tp);
+        case 3: return pick_sample<3>(np, multi, tp);
+        case 6: return pick_sample<6>(np, multi, tp);
+        case 7: return pick_sample<7>(np, multi, tp);
+        case 14: return pick_sample<14>(np, multi, tp);
+        case 15: return pick_sample<15>(np, multi, tp);
+        default: return nullptr;
+    }
+}
+#else
 
 int check_gfx950(int dev) {
     hipDeviceProp_t prop;
@@ -1257,12 +1280,13 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->t0 = t0;
     h->launch = pick_ll(n_planets, n_inst > 1, 0, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample = pick_sample<1>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_fused[0] = pick_sample<2>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_eval[0] = pick_sample<3>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_fused[1] = pick_sample<6>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_eval[1] = pick_sample<7>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_fused[2] = pick_sample<14>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_eval[2] = pick_sample<15>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    // (the proposal-making modes live in rvk_sample.hip's build of this file)
+    h->sample_fused[0] = pick_sample_fused(2, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_eval[0] = pick_sample_fused(3, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_fused[1] = pick_sample_fused(6, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_eval[1] = pick_sample_fused(7, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_fused[2] = pick_sample_fused(14, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    h->sample_eval[2] = pick_sample_fused(15, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_direct[0] = pick_sample<19>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_direct[1] = pick_sample<23>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_direct[2] = pick_sample<31>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
@@ -1535,3 +1559,4 @@ int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, 
 }
 
 }  // extern "C"
+#endif  // RVK_TU_SAMPLE

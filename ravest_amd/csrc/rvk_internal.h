@@ -61,6 +61,9 @@ typedef void (*loglike_launch_t)(hipStream_t, EpochData, int, int, const double 
 
 typedef void (*sample_launch_t)(hipStream_t, EpochData, int, int, const double *, long long, long long, PostArgs,
                                 const SampleArgs &);
+// the launcher of the fused half-step kernels of one MODE (2, 3, 6, 7, 14, 15: rvk.hip's
+// pick_sample_s), defined in rvk_sample.hip's build of rvk.hip; nullptr when the shape has none
+sample_launch_t pick_sample_fused(int mode, int np, bool multi, bool tp);
 
 int fail(int code, const std::string &msg);
 

@@ -8,14 +8,16 @@ set -e
 cd "$(dirname "$0")/.."
 OUT=${VAROUT:-varlib}
 mkdir -p $OUT
-ALL="rvk rvk_post rvk_gp rvk_gp64"
+ALL="rvk rvk_sample rvk_post rvk_gp rvk_gp64"
 TUS=${TUS:-$ALL}
 one() {
   local name=$1 flags=$2 o=build/var/$1 objs=""
   mkdir -p $o
   for s in $ALL; do
     if [[ " $TUS " == *" $s "* ]]; then
-      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result $flags -c \
+      local tuf=""
+      [ $s = rvk_sample ] && tuf="-mllvm -amdgpu-sched-strategy=iterative-ilp"   # as the Makefile
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result $tuf $flags -c \
         -o $o/$s.o ravest_amd/csrc/$s.hip -Rpass-analysis=kernel-resource-usage 2> $o/$s.res &
       objs="$objs $o/$s.o"
     else
