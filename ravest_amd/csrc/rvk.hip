@@ -28,6 +28,10 @@
 #include "rvk_internal.h"
 #include "rvk_post_dev.h"
 
+#ifndef RVK_TU_SAMPLE
+#define RVK_TU_SAMPLE 0   // 1 / 2: rvk_sample.hip / rvk_sample1.hip's builds of this file (the fused half-steps)
+#endif
+
 using namespace rvk;
 
 namespace {
@@ -1042,12 +1046,21 @@ sample_launch_t pick_sample_s(int np) {
             default: return np <= RVK_MAX_PLANETS ? launch_sample<0, MULTI, TP> : nullptr;
         }
     } else {
-        switch (np) {
-            case 1: return launch_sample_fused<1, MULTI, TP, MODE>;
-            case 2: return launch_sample_fused<2, MULTI, TP, MODE>;
-            case 3: return launch_sample_fused<3, MULTI, TP, MODE>;
-            case 4: return launch_sample_fused<4, MULTI, TP, MODE>;
-            default: return nullptr;
+        // one planet with the basic priors (MODE 2 / 3) is rvk_sample1.hip's (RVK_TU_SAMPLE 2), the
+        // other shapes rvk_sample.hip's (RVK_TU_SAMPLE 1): each build instantiates only its own
+        constexpr bool NP1 = MODE == 2 || MODE == 3;
+        if constexpr (RVK_TU_SAMPLE == 2) {
+            return np == 1 && NP1 ? launch_sample_fused<1, MULTI, TP, MODE> : nullptr;
+        } else {
+            switch (np) {
+                case 1:
+                    if constexpr (NP1 && RVK_TU_SAMPLE == 1) return nullptr;
+                    else return launch_sample_fused<1, MULTI, TP, MODE>;
+                case 2: return launch_sample_fused<2, MULTI, TP, MODE>;
+                case 3: return launch_sample_fused<3, MULTI, TP, MODE>;
+                case 4: return launch_sample_fused<4, MULTI, TP, MODE>;
+                default: return nullptr;
+            }
         }
     }
 }
@@ -1061,11 +1074,22 @@ sample_launch_t pick_sample(int np, bool multi, bool tp) {
 #if RVK_TU_SAMPLE
 }  // namespace
 
-// rvk_sample.hip compiles this file a second time with RVK_TU_SAMPLE: only the kernels that make
-// their own stretch-move proposals (MODE 2 / 3, | 4, | 8), under the iterative-ILP machine scheduler
-// (Makefile).  Measured (session r5flags, tools/sampler_variants.py, 3 interleaved reps): the
-// half-steps 1.5 % (uniform priors) to 6.5 % (VanEylen) faster with it, while the plain likelihood
-// kernels lose 1-3.5 % (tools/kbench.py), so they keep the default scheduler in rvk.hip.
+// rvk_sample.hip and rvk_sample1.hip compile this file again with RVK_TU_SAMPLE 1 / 2: only the
+// kernels that make their own stretch-move proposals (MODE 2 / 3, | 4, | 8), under other machine
+// schedulers (Makefile).  Measured (sessions r5flags / r5tu / r5st, tools/sampler_variants.py, 3
+// interleaved reps): iterative-ILP makes the half-steps 1.6 % (uniform priors) to 7 % (VanEylen)
+// faster, max-ILP the one-planet basic-prior half-step (the config-2 sampler) 2.7 % faster again but
+// the others ~1 % slower; the plain likelihood kernels lose 1-3.5 % under either (tools/kbench.py),
+// so they keep the default scheduler in rvk.hip.
+#if RVK_TU_SAMPLE == 2
+rvk::sample_launch_t rvk::pick_sample_fused_np1(int mode, bool multi, bool tp) {
+    switch (mode) {
+        case 2: return pick_sample<2>(1, multi, tp);
+        case 3: return pick_sample<3>(1, multi, tp);
+        default: return nullptr;
+    }
+}
+#else
 rvk::sample_launch_t rvk::pick_sample_fused(int mode, int np, bool multi, bool tp) {
     switch (mode) {
         case 2: return pick_sample<2>(np, multi, tp);
@@ -1077,6 +1101,7 @@ rvk::sample_launch_t rvk::pick_sample_fused(int mode, int np, bool multi, bool t
         default: return nullptr;
     }
 }
+#endif
 #else
 
 int check_gfx950(int dev) {
@@ -1280,13 +1305,18 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     h->t0 = t0;
     h->launch = pick_ll(n_planets, n_inst > 1, 0, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample = pick_sample<1>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    // (the proposal-making modes live in rvk_sample.hip's build of this file)
-    h->sample_fused[0] = pick_sample_fused(2, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_eval[0] = pick_sample_fused(3, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_fused[1] = pick_sample_fused(6, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_eval[1] = pick_sample_fused(7, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_fused[2] = pick_sample_fused(14, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
-    h->sample_eval[2] = pick_sample_fused(15, n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
+    // (the proposal-making modes live in rvk_sample.hip's and rvk_sample1.hip's builds of this file)
+    const bool multi = n_inst > 1, tpi = RVK_TP_INLINE && par == RVK_PAR_PKEWTP;
+    auto fused = [&](int mode) {
+        return n_planets == 1 && (mode == 2 || mode == 3) ? pick_sample_fused_np1(mode, multi, tpi)
+                                                          : pick_sample_fused(mode, n_planets, multi, tpi);
+    };
+    h->sample_fused[0] = fused(2);
+    h->sample_eval[0] = fused(3);
+    h->sample_fused[1] = fused(6);
+    h->sample_eval[1] = fused(7);
+    h->sample_fused[2] = fused(14);
+    h->sample_eval[2] = fused(15);
     h->sample_direct[0] = pick_sample<19>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_direct[1] = pick_sample<23>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);
     h->sample_direct[2] = pick_sample<31>(n_planets, n_inst > 1, RVK_TP_INLINE && par == RVK_PAR_PKEWTP);

@@ -64,6 +64,8 @@ typedef void (*sample_launch_t)(hipStream_t, EpochData, int, int, const double *
 // the launcher of the fused half-step kernels of one MODE (2, 3, 6, 7, 14, 15: rvk.hip's
 // pick_sample_s), defined in rvk_sample.hip's build of rvk.hip; nullptr when the shape has none
 sample_launch_t pick_sample_fused(int mode, int np, bool multi, bool tp);
+// MODE 2 / 3 with one planet, from rvk_sample1.hip's build
+sample_launch_t pick_sample_fused_np1(int mode, bool multi, bool tp);
 
 int fail(int code, const std::string &msg);
 

@@ -8,8 +8,7 @@ REV=${1:-HEAD}; NAME=${2:-head}
 WT=$(mktemp -d /tmp/rvk_ab.XXXX)
 git worktree add -q --detach "$WT" "$REV"
 mkdir -p build/variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o build/variants/librvk_$NAME.so \
-  "$WT"/ravest_amd/csrc/rvk.hip "$WT"/ravest_amd/csrc/rvk_post.hip "$WT"/ravest_amd/csrc/rvk_gp.hip \
-  "$WT"/ravest_amd/csrc/rvk_gp64.hip
+make -s -j4 -C "$WT"/ravest_amd > /dev/null   # the committed Makefile (its translation units and flags)
+cp "$WT"/ravest_amd/lib/librvk.so build/variants/librvk_$NAME.so
 git worktree remove --force "$WT"
 ls -la build/variants/librvk_$NAME.so

@@ -8,7 +8,7 @@ set -e
 cd "$(dirname "$0")/.."
 OUT=${VAROUT:-varlib}
 mkdir -p $OUT
-ALL="rvk rvk_sample rvk_post rvk_gp rvk_gp64"
+ALL="rvk rvk_sample rvk_sample1 rvk_post rvk_gp rvk_gp64"
 TUS=${TUS:-$ALL}
 one() {
   local name=$1 flags=$2 o=build/var/$1 objs=""
@@ -16,7 +16,10 @@ one() {
   for s in $ALL; do
     if [[ " $TUS " == *" $s "* ]]; then
       local tuf=""
-      [ $s = rvk_sample ] && tuf="-mllvm -amdgpu-sched-strategy=iterative-ilp"   # as the Makefile
+      if [[ "$flags" != *sched-strategy* ]]; then   # as the Makefile
+        [ $s = rvk_sample ] && tuf="-mllvm -amdgpu-sched-strategy=iterative-ilp"
+        [ $s = rvk_sample1 ] && tuf="-mllvm -amdgpu-sched-strategy=max-ilp"
+      fi
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result $tuf $flags -c \
         -o $o/$s.o ravest_amd/csrc/$s.hip -Rpass-analysis=kernel-resource-usage 2> $o/$s.res &
       objs="$objs $o/$s.o"
