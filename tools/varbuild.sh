@@ -10,6 +10,7 @@ OUT=${VAROUT:-varlib}
 mkdir -p $OUT
 ALL="rvk rvk_sample rvk_sample1 rvk_post rvk_gp rvk_gp64"
 TUS=${TUS:-$ALL}
+for t in $TUS; do [[ " $ALL " == *" $t "* ]] || ALL="$ALL $t"; done   # a unit only the variant has
 one() {
   local name=$1 flags=$2 o=build/var/$1 objs=""
   mkdir -p $o
