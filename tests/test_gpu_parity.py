@@ -276,3 +276,42 @@ def test_lanes_per_walker_layouts_vs_oracle(lpw, np_, ni, n, par, trend):
     eng.set_lanes_per_walker(64)
     assert np.array_equal(np.isfinite(ll2), np.isfinite(eng.loglike(big)))
     assert_ll_close(ll2, eng.loglike(big), what=f"lpw{lpw}-vs-64-big")
+
+
+def _random_shapes(count=24, seed=2025):
+    """Seeded random shapes across the launch paths: 1-12 planets (the fixed-NP kernels and the
+    generic one), 1-6 instruments, epoch counts around the wave and tile edges (1 .. 1100), walker
+    counts around the block and lane-layout edges (1 .. 4100), every parameterisation, trend on/off."""
+    rng = np.random.default_rng(seed)
+    pars = ["P K e w Tp", "P K e w Tc", "P K secosw sesinw Tp", "P K secosw sesinw Tc"]
+    out = []
+    for k in range(count):
+        np_ = int(rng.choice([1, 1, 1, 2, 3, 4, 5, 8, 9, 12]))
+        n = int(rng.choice([1, 2, 31, 63, 64, 65, 127, 255, 256, 513, 1100]))
+        ni = int(min(n, rng.integers(1, 7)))
+        W = int(rng.choice([1, 3, 63, 64, 65, 255, 1000, 4100]))
+        while W * n * np_ > 5_000_000:
+            W = max(1, W // 2)
+        out.append((k, np_, ni, n, W, pars[k % 4], bool(rng.integers(2))))
+    return out
+
+
+@pytest.mark.parametrize("k,np_,ni,n,W,par,trend", _random_shapes())
+def test_random_shapes_vs_oracle(k, np_, ni, n, W, par, trend):
+    """Randomised shape sweep (seeded): the host-buffer and the device-resident entry points
+    against the C oracle at the stated tolerance, identical -inf masks, and the two entry points
+    bitwise equal to each other."""
+    import torch
+    from oracle import oracle
+    from ravest_amd.engine import RVEngine
+    from ravest_amd.synth import make_dataset, make_walkers
+    ds = make_dataset(np_, n, ni, seed=300 + k, parameterisation=par, trend=trend)
+    th = make_walkers(ds, W, seed=400 + k)
+    eng = RVEngine(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation, ds.t0)
+    ll = eng.loglike(th)
+    ref, _ = oracle.loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, ni, np_, ds.parameterisation.code, ds.t0, th)
+    assert_ll_close(ll, ref, what=f"shape{k}-np{np_}-ni{ni}-n{n}-W{W}")
+    out = torch.empty(W, dtype=torch.float64, device="cuda")
+    eng.loglike_device(torch.from_numpy(th).cuda(), out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), ll.view(np.uint64))
