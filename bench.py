@@ -49,6 +49,11 @@ def parse():
     ap.add_argument("--group", action="store_true",
                     help="start the process group and take the N>1 code path (RCCL all-gathers) even at N=1")
     ap.add_argument("--graph-steps", type=int, default=50, help="steps captured per HIP graph")
+    ap.add_argument("--gather", choices=["graph", "stream", "none"], default="graph",
+                    help="N>1 (RCCL): the K launches and the all-gathers captured in one HIP graph (default) "
+                         "or issued from the host per group")
+    ap.add_argument("--gather-steps", type=int, default=None,
+                    help="N>1: steps whose log-probs one all-gather carries (default K: one gather per region)")
     ap.add_argument("--streams", type=int, default=1, help="independent streams per graph (--launch graph)")
     ap.add_argument("--launch", choices=["eager", "graph"], default="graph",
                     help="timed loop: G-step HIP graph replays (default) or back-to-back stream launches")
@@ -276,8 +281,8 @@ def config4_sharded_line(world: int, rank: int, backend: str, grouped: bool = Fa
     """Config 4 as BASELINE names it: 65536 walkers (2 planets x 512 epochs) split over the N
     ranks (strong scaling, 65536/N contiguous walkers each) by ShardedDevicePosterior: each rank
     launches rvk_loglike_device on its slice and the per-walker log-probs are all-gathered (RCCL
-    over xGMI) into every rank's [65536] buffer.  Timed: reps x (launch + all-gather), barrier +
-    sync on both sides, max over ranks.  Checked: the gathered block equals rank 0's own single
+    over xGMI) into every rank's [65536] buffer.  Timed: reps x (launch + all-gather) from a
+    common start (barrier + sync) to each rank's own synchronize, max over ranks.  Checked: the gathered block equals rank 0's own single
     evaluation of all 65536 walkers, bit for bit."""
     import torch
     import torch.distributed as dist
@@ -304,9 +309,7 @@ def config4_sharded_line(world: int, rank: int, backend: str, grouped: bool = Fa
     for _ in range(reps):
         sh(th, out)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    el = time.perf_counter() - t0                    # this rank's end; max over ranks below
     ref = torch.empty(Wt, dtype=torch.float64, device=dev)
     eng.loglike_device(th, ref)
     torch.cuda.synchronize(dev)
@@ -513,7 +516,7 @@ def config4_sampler_line(world: int, rank: int, backend: str, grouped: bool = Fa
     """Config 4 as a sampler: 65536 walkers (2 planets x 512 epochs, 14 free parameters).  N = 1:
     DeviceEnsembleSampler's kernel (rvk_stretch_run, one fused kernel per half-step); N > 1:
     ShardedDeviceSampler (each rank evaluates 32768 / N proposals per half-step, the 32768
-    log-posteriors all-gathered: 256 KB per half-step), run_mcmc timed with barriers, max over
+    log-posteriors all-gathered: 256 KB per half-step), run_mcmc timed from a common start (barrier) to each rank's own end, max over
     ranks, chain kept on rank 0's host."""
     import torch
     import torch.distributed as dist
@@ -534,8 +537,7 @@ def config4_sampler_line(world: int, rank: int, backend: str, grouped: bool = Fa
     t0 = time.perf_counter()
     s.run_mcmc(None, steps)
     torch.cuda.synchronize()
-    dist.barrier()
-    el = time.perf_counter() - t0
+    el = time.perf_counter() - t0                    # this rank's end; max over ranks below
     t = torch.tensor([el], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms = float(t[0]) / steps * 1e3
@@ -684,6 +686,178 @@ def predictive_line(eng, theta, S: int = 100_000, T: int = 1000, reps: int = 5) 
                                  "samples + 8*T times per launch / launch time"}}
 
 
+def n1_steps(args, eng, th_d, W: int, dev, ll):
+    """The N = 1 timed loop.  graph (default): G-step HIP graphs replayed (S independent streams
+    per graph); eager: K stream-ordered launches issued back to back through the C-ABI entry point
+    (ctypes call pre-bound).  Measured on MI355X, config 2: at K = 20 (one replay) graph 8.6-8.7 us
+    vs eager 8.9 us wall per step (eager's kernels run 0.25 us shorter, its host issue costs
+    more); at K = 200 both 7.6 us.  Returns (elapsed s, kernel ms: HIP events around each group
+    of G launches in the timed region / G, G)."""
+    import torch
+    stream = torch.cuda.current_stream(dev)
+    G = max(1, min(args.graph_steps, args.steps))
+    while args.steps % G:                            # time exactly K steps
+        G -= 1
+    S = max(1, args.streams)
+    outs = torch.empty(G, W, dtype=torch.float64, device=dev)
+    from ravest_amd import _lib
+    ll_fn = _lib.load().rvk_loglike_device
+    call_args = [(eng._h, th_d.data_ptr(), W, th_d.stride(0), outs[j].data_ptr(), stream.cuda_stream)
+                 for j in range(G)]
+
+    def run_group():
+        for a in call_args:
+            if ll_fn(*a):
+                _lib.check(-1)
+
+    if args.launch == "graph":
+        cap = torch.cuda.Stream(dev)
+        side = [torch.cuda.Stream(dev) for _ in range(S)]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            for st in side:
+                st.wait_stream(cap)
+            for j in range(G):
+                eng.loglike_device(th_d, outs[j], side[j % S])
+            for st in side:
+                cap.wait_stream(st)
+        g.replay()                                   # warm replay
+        launch_group = g.replay                      # replayed on `stream`
+    else:
+        launch_group = run_group
+    launch_group()
+    torch.cuda.synchronize(dev)
+    if not np.array_equal(outs[G - 1].cpu().numpy(), ll):
+        raise RuntimeError("timed-loop launch result differs from the first eager launch")
+    out1 = torch.empty(W, dtype=torch.float64, device=dev)
+    for _ in range(max(1, args.warmup)):             # the W untimed warmup steps, right before the region
+        eng.loglike_device(th_d, out1, stream)
+    rep_ev = []
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps // G):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        launch_group()
+        b.record(stream)
+        rep_ev.append((a, b))
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    kern_ms = float(sum(a.elapsed_time(b) for a, b in rep_ev)) / args.steps
+    return el, kern_ms, G
+
+
+def grouped_steps(args, eng, th_d, W: int, world: int, backend: str, dev) -> dict:
+    """The N > 1 timed loop (weak scaling; also run at world 1 by --group).
+
+    K steps in R = K / G groups of G launches; after each group its G x W log-probs are
+    all-gathered (RCCL over xGMI) into a buffer of their own (no buffer is reused inside the
+    region, so no gather waits for an earlier one).  Default G = K: ONE all-gather of all K
+    steps' log-probs at the end of the region.  --gather graph (the default with RCCL): the
+    whole region -- the K launches on one stream and the R all-gathers on RCCL's stream -- is
+    captured once into one HIP graph and the timed region is one replay, so the host issues one
+    call instead of K launches and R collectives.  --gather stream: the same work issued from
+    the host every region (one G-launch graph replay + one async all-gather per group).  gloo
+    (the 1-GPU rehearsal): stream form, gathers staged through host memory.  --gather none: the
+    graph without the gathers (probe only; the bitwise check then fails by construction).
+    Measured at RCCL world 1 on one MI355X (tools/group_sweep.sh, profiles/round6/): graph, G = 20
+    8.39-8.68 us per step against 8.68-9.32 for the N = 1 line of the same session; each further
+    gather inside the graph adds ~20-25 us per region (G = 10: 10.3-11.5, G = 5: 12.3-14.4, G = 2:
+    16.6-17.5) although the gather itself is a 3 us copy at world 1 -- the cost is the forked
+    branch's cross-queue dependencies, not the bytes; host-issued (stream, G = 20) 10.6-10.8.
+
+    Timing: the region starts at a common point (barrier + synchronize on every rank, then
+    each rank's clock), ends on each rank when its own stream work (kernels and gathers) has
+    completed (synchronize), and the elapsed times are MAX-reduced after the region -- no
+    collective other than the gathers inside it.  kernel_ms: HIP events around a K-launch
+    graph of the kernel alone on this rank's stream, replayed right before the region (the
+    gather kernels would overlap events inside the captured region)."""
+    import torch
+    import torch.distributed as dist
+    K = args.steps
+    G = min(args.gather_steps or K, K)
+    while K % G:
+        G -= 1
+    R = K // G
+    mode = args.gather if backend == "nccl" else "stream"
+    stream = torch.cuda.current_stream(dev)
+    outs = [torch.empty(G, W, dtype=torch.float64, device=dev) for _ in range(R)]
+    gath = [torch.empty(world * G * W, dtype=torch.float64, device=dev) for _ in range(R)]
+    cap = torch.cuda.Stream(dev)
+
+    def issue_all(st):
+        """K launches on `st` and R async all-gathers (the current stream must be `st`)."""
+        works = []
+        for r in range(R):
+            for j in range(G):
+                eng.loglike_device(th_d, outs[r][j], st)
+            if mode != "none":                        # "none": the same graph without the gathers (probe)
+                works.append(dist.all_gather_into_tensor(gath[r], outs[r].view(-1), async_op=True))
+        for w in works:
+            w.wait()
+
+    # warm every gather buffer and RCCL's channels eagerly (the communicator exists already:
+    # init_process_group(device_id=...) initialises it eagerly)
+    if backend == "nccl":
+        with torch.cuda.stream(cap):
+            issue_all(cap)
+        torch.cuda.synchronize(dev)
+
+    graph = None
+    if mode in ("graph", "none"):
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
+                issue_all(cap)
+            graph.replay()                            # warm replay
+            torch.cuda.synchronize(dev)
+            region = graph.replay
+        except Exception as e:                        # capture of the collective refused: host-issued form
+            print(f"bench.py: HIP-graph capture of the all-gather failed ({e}); using --gather stream",
+                  file=sys.stderr, flush=True)
+            graph, mode = None, "stream"
+            torch.cuda.synchronize(dev)
+    if graph is None:
+        gg = []
+        for r in range(R):                            # G-launch kernel graphs, one per output buffer
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                for j in range(G):
+                    eng.loglike_device(th_d, outs[r][j], cap)
+            gg.append(g)
+        for g in gg:
+            g.replay()
+        torch.cuda.synchronize(dev)
+
+        def region():
+            works = []
+            for r in range(R):
+                gg[r].replay()
+                if backend == "nccl":
+                    works.append(dist.all_gather_into_tensor(gath[r], outs[r].view(-1), async_op=True))
+                else:
+                    hb = torch.empty(world * G * W, dtype=torch.float64)
+                    dist.all_gather_into_tensor(hb, outs[r].view(-1).cpu())
+                    gath[r].copy_(hb)
+            for w in works:
+                w.wait()
+
+    kern_ms = graph_kernel_ms(lambda st: eng.loglike_device(th_d, outs[0][0], st), G=K)
+    out1 = torch.empty(W, dtype=torch.float64, device=dev)
+    for _ in range(max(1, args.warmup)):             # the W untimed warmup steps, right before the region
+        eng.loglike_device(th_d, out1, stream)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    region()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"el": float(t[0]), "kern_ms": float(t[1]), "G": G, "R": R, "mode": mode,
+            "last": gath[R - 1].view(world, G, W)[:, G - 1, :].reshape(-1)}
+
+
 def main():
     args = parse()
     import torch
@@ -746,112 +920,27 @@ def main():
     host_ms = None if args.no_host_path else _med_us(lambda: eng.loglike(theta), 200) * 1e-3
 
     # ---- the timed steps -------------------------------------------------------------------
-    # graph (default): G-step HIP graphs replayed (S independent streams per graph); eager: K
-    # stream-ordered launches issued back to back through the C-ABI entry point (ctypes call
-    # pre-bound).  Measured on MI355X, config 2: at K = 20 (one replay) graph 8.6-8.7 us vs
-    # eager 8.9 us wall per step (eager's kernels run 0.25 us shorter, its host issue costs
-    # more); at K = 200 both 7.6 us.  N > 1: one all-gather of the G steps' log-probs every G steps.
-    # N > 1: a quarter of the steps per group (the driver's K = 20: 4 groups of 5), so the
-    # all-gather of group r overlaps group r+1's launches and only the last one is exposed
-    G = max(1, min(args.graph_steps, args.steps if not grouped else max(1, args.steps // 4)))
-    while args.steps % G:                            # time exactly K steps
-        G -= 1
-    S = max(1, args.streams)
-    nset = 2                                         # two output sets: group r+1 overlaps gather r
-    outs = [torch.empty(G, W, dtype=torch.float64, device=dev) for _ in range(nset)]
-    gath = [torch.empty(world * G * W, dtype=torch.float64, device=dev) for _ in range(nset)] if grouped else None
-    from ravest_amd import _lib
-    ll_fn = _lib.load().rvk_loglike_device
-    call_args = [[(eng._h, th_d.data_ptr(), W, th_d.stride(0), outs[k][j].data_ptr(), stream.cuda_stream)
-                  for j in range(G)] for k in range(nset)]
-
-    def run_group(k):
-        for a in call_args[k]:
-            if ll_fn(*a):
-                _lib.check(-1)
-
-    graphs = []
-    if args.launch == "graph":
-        cap = torch.cuda.Stream(dev)
-        side = [torch.cuda.Stream(dev) for _ in range(S)]
-        for k in range(nset):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=cap):
-                for st in side:
-                    st.wait_stream(cap)
-                for j in range(G):
-                    eng.loglike_device(th_d, outs[k][j], side[j % S])
-                for st in side:
-                    cap.wait_stream(st)
-            graphs.append(g)
-        for g in graphs:                             # warm replays
-            g.replay()
-        launch_group = lambda k: graphs[k].replay()   # noqa: E731  (replayed on `stream`)
-    else:
-        launch_group = run_group
-    for k in range(nset):
-        launch_group(k)
-    torch.cuda.synchronize(dev)
-    if not np.array_equal(outs[0][G - 1].cpu().numpy(), ll):
-        raise RuntimeError("timed-loop launch result differs from the first eager launch")
-    for _ in range(max(1, args.warmup)):             # the W untimed warmup steps, right before the region
-        eng.loglike_device(th_d, out1, stream)
-
-    works = [None] * nset
-    rep_ev = []
-    if grouped:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    done = 0
-    r = 0
-    while done < args.steps:
-        k = r % nset
-        if works[k] is not None:                     # set k's previous gather must have read it
-            works[k].wait()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        launch_group(k)
-        b.record(stream)
-        rep_ev.append((a, b))
-        if grouped and backend == "nccl":
-            works[k] = dist.all_gather_into_tensor(gath[k], outs[k].view(-1), async_op=True)
-        elif grouped:
-            hb = torch.empty(world * G * W, dtype=torch.float64)
-            dist.all_gather_into_tensor(hb, outs[k].view(-1).cpu())
-            gath[k].copy_(hb)
-        done += G
-        r += 1
-    for k in range(nset):
-        if works[k] is not None:
-            works[k].wait()
-    torch.cuda.synchronize(dev)
-    if grouped:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    steps_run = done
-    # average kernel duration inside the timed region: G back-to-back launches per event pair
-    kern_ms = float(sum(a.elapsed_time(b) for a, b in rep_ev)) / steps_run
-    if grouped:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_ms = float(t[0]), float(t[1])
+    G, S, gmode = None, max(1, args.streams), None
     ranks_same = None
     if grouped:
+        res = grouped_steps(args, eng, th_d, W, world, backend, dev)
+        el, kern_ms, G, gmode = res["el"], res["kern_ms"], res["G"], res["mode"]
         # every rank's results, as gathered, against THIS rank's own single launch over all
         # world x W walkers (a different batch size, so possibly a different lane layout):
         # bitwise identical means the shard split changes nothing
-        got = gath[(r - 1) % nset].view(world, G, W)[:, G - 1, :].reshape(-1).cpu().numpy()
+        got = res["last"].cpu().numpy()
         th_all = torch.from_numpy(theta_all).to(dev)
         ref_all = torch.empty(world * W, dtype=torch.float64, device=dev)
         eng.loglike_device(th_all, ref_all, stream)
         torch.cuda.synchronize(dev)
-        bad = 0.0 if np.array_equal(got, ref_all.cpu().numpy()) else 1.0
+        bad = 0.0 if np.array_equal(got, ref_all.cpu().numpy()) and np.array_equal(got[rank * W:(rank + 1) * W], ll) \
+            else 1.0
         t = torch.tensor([bad], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ranks_same = bool(t[0] == 0.0)
         del th_all, ref_all
-    args.steps = steps_run
+    else:
+        el, kern_ms, G = n1_steps(args, eng, th_d, W, dev, ll)
 
     solves = W * n_ep * n_pl * args.steps * world
     value = solves / el
@@ -878,8 +967,11 @@ def main():
             "kernel_ms": kern_ms,
             "eager_event_ms": eager_ms,
             "host_path_ms_per_call": host_ms,
-            "launch": (f"{G}-step HIP graphs, {S} streams" if args.launch == "graph" else
-                       "back-to-back stream launches") + (f", 1 all-gather per {G} steps" if world > 1 else ""),
+            "launch": ((f"{G}-step HIP graphs, {S} streams" if args.launch == "graph" else
+                        "back-to-back stream launches") if not grouped else
+                       (f"all {args.steps} launches + {args.steps // G} all-gathers (one per {G} steps) captured in one "
+                        "HIP graph, one replay" if gmode == "graph" else
+                        f"{G}-step HIP graph replays, 1 async all-gather per {G} steps issued from the host")),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "achieved_per_step": alg_bytes / (el / args.steps) / 1e9,
@@ -918,9 +1010,11 @@ def main():
             line["config4_sampler"] = c4s
     if rank == 0:
         if grouped:
-            line["process_group"] = {"backend": backend, "world_size": world,
-                                     "note": "timed loop with the N>1 path: async all-gather of each group's "
-                                             "log-probs, double-buffered"}
+            line["process_group"] = {"backend": backend, "world_size": world, "gather": gmode,
+                                     "note": "timed loop with the N>1 path (grouped_steps): each group's log-probs "
+                                             "all-gathered into a buffer of its own; the region starts after a "
+                                             "barrier + synchronize, ends at each rank's own synchronize, max over "
+                                             "ranks; kernel_ms from a kernel-only K-launch graph before the region"}
         print(json.dumps(line), flush=True)
     if grouped:
         dist.destroy_process_group()

@@ -146,12 +146,15 @@ int rvk_solve_kepler(const double *M, const double *e, int64_t n, double *cosE, 
 #define RVK_HOSTIO_PAGEABLE  1
 #define RVK_HOSTIO_PINNED    2
 #define RVK_HOSTIO_ZEROCOPY  3
-/* RVK_OPT_LDS_POISON (tests only; default 0): every kernel that stages the sin/cos table in
- * LDS first writes each entry as NaN and the real value ~10 us later, before the barrier
+/* RVK_OPT_LDS_POISON (tests only; default 0): every kernel LAUNCHED FOR A HANDLE (likelihood,
+ * log-posterior, sampler, predictive, GP) that stages the sin/cos table in LDS first writes
+ * each entry as NaN and the real value ~10 us later, before the barrier
  * that publishes the table.  A read of the table that is not ordered after that barrier
  * then sees NaN and the results are NaN: the GPU parity tests run with it on to catch a
  * publish-order race (round 4 found one that green tests had missed).  Same results when
- * the kernels are race-free; slower. */
+ * the kernels are race-free; slower.  rvk_solve_kepler (no handle) does not take it.
+ * Value 2 (the tests' positive control): the real value is never stored, every table read
+ * is NaN, so the results of every kernel the option reaches are NaN. */
 #define RVK_OPT_LDS_POISON 5
 int rvk_set_option(rvk_handle *h, int32_t key, int32_t value);
 

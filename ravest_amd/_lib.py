@@ -12,7 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _DEFAULT_PATH = LIB_PATH = os.path.join(_HERE, "lib", "librvk.so")
-# experiment hook: A/B builds of the same source (tools/variants.sh); never set in production
+# experiment hook: A/B builds (tools/varbuild.sh, tools/ab_rev.sh); never set in production
 LIB_PATH = os.environ.get("RAVEST_AMD_LIB", LIB_PATH)
 
 # every symbol declared in include/rvk.h, include/rvk_post.h and include/rvk_gp.h

@@ -1381,7 +1381,7 @@ int rvk_set_option(rvk_handle *h, int32_t key, int32_t value) {
         return RVK_OK;
     }
     if (key == RVK_OPT_LDS_POISON) {
-        if (value != 0 && value != 1) return fail(RVK_E_ARG, "lds poison must be 0 or 1");
+        if (value < 0 || value > 2) return fail(RVK_E_ARG, "lds poison must be 0, 1 or 2");
         h->poison = value;
         return RVK_OK;
     }

@@ -984,11 +984,17 @@ static void free_gp(rvk_gp *g) {
     delete g;
 }
 
-// LDS a workgroup may allocate on this device (gfx950: 160 KB; the runtime reports it as the
-// per-CU or the per-block figure, whichever it fills in).
+// LDS per CU on this device (gfx950: 160 KB; the runtime reports it as the per-CU or the
+// per-block figure, whichever it fills in): the fp32 occupancy estimate only.
 static size_t lds_per_cu(const hipDeviceProp_t &prop) {
     const size_t a = prop.maxSharedMemoryPerMultiProcessor, b = prop.sharedMemPerBlock;
     return a > b ? a : b;
+}
+
+// LDS ONE workgroup may allocate (the launch limit): the per-block figure, the per-CU one only
+// when the runtime leaves the per-block figure at 0.
+static size_t lds_per_block(const hipDeviceProp_t &prop) {
+    return prop.sharedMemPerBlock ? (size_t)prop.sharedMemPerBlock : (size_t)prop.maxSharedMemoryPerMultiProcessor;
 }
 
 // The fp32 factorisation's launch shape and workspace (n <= kGpF32MaxEpochs: its column panel
@@ -1032,9 +1038,9 @@ static int create_gp(rvk_gp *g, rvk_handle *h, int32_t kernel) {
     g->cond64 = pick_gp64(h->n_planets, h->n_inst > 1, h->par == RVK_PAR_PKEWTP, true, s64);
     if (!g->launch64 || !g->cond64) return fail(RVK_E_ARG, "GP supports 1..32 planets");
     g->lds64 = gp64_lds_bytes(h->n, h->n_planets, s64.nw);
-    if (g->lds64 > lds_per_cu(prop))
+    if (g->lds64 > lds_per_block(prop))
         return fail(RVK_E_ARG, "GP fp64 kernel: LDS need (" + std::to_string(g->lds64) + " B) exceeds the device's " +
-                                   std::to_string(lds_per_cu(prop)) + " B per workgroup");
+                                   std::to_string(lds_per_block(prop)) + " B per workgroup");
     g->grid64 = (unsigned)prop.multiProcessorCount;
     g->w64stride = gp64_work_doubles(h->n);
     HIPCHK(hipMalloc(&g->d_work64, sizeof(double) * (size_t)g->w64stride * g->grid64));

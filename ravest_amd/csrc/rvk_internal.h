@@ -34,13 +34,16 @@ struct EpochData {
 
 // Store entry i of an LDS copy of the sin/cos table.  poison (RVK_OPT_LDS_POISON, tests only):
 // NaN first, the real value ~10 us later (the compiler barrier keeps the first store), so a
-// reader not ordered after the publishing barrier sees NaN.
+// reader not ordered after the publishing barrier sees NaN.  poison == 2 (the tests' positive
+// control): the real value is never stored, so every table read is NaN -- a kernel the option
+// reaches then returns NaN walkers, which shows the equality tests run poisoned.
 __device__ __forceinline__ void tab_put(SC *tab, int i, SC v, int poison) {
     if (poison) {
         tab[i] = SC{__builtin_nan(""), __builtin_nan("")};
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         for (int k = 0; k < 3; ++k) __builtin_amdgcn_s_sleep(127);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (poison > 1) return;
     }
     tab[i] = v;
 }

@@ -343,13 +343,43 @@ class ShardedDeviceSampler(_DevicePipeline):
 
     def get_autocorr_time(self, discard=0, thin=1, **kwargs):
         """emcee's estimate.  keep_chain="all": computed locally on each rank (every rank holds the
-        same chain bits in the same storage, so the estimates are equal; no collective).  One
-        keeping rank: computed there and broadcast (collective: call it on every rank, as
-        ravest's convergence loop does), so a convergence test cannot break on one rank and not
-        on another."""
+        same chain bits in the same storage, so the estimates should be equal), then one small
+        guard collective: a MAX all-reduce of [tau, -tau, failed] that raises on EVERY rank if
+        the ranks' estimates differ in any bit (e.g. a different FFT plan on one GPU) or the
+        estimate failed on any rank -- so a convergence test cannot break on one rank and not on
+        another and leave the others waiting in the next all-gather.  One keeping rank: computed
+        there and broadcast.  Both forms are collective: call it on every rank, as ravest's
+        convergence loop does."""
         import torch
-        if not self.grouped or self.keep_chain == "all":
+        if not self.grouped:
             return super().get_autocorr_time(discard=discard, thin=thin, **kwargs)
+        if self.keep_chain == "all":
+            from .sampler import AutocorrError
+            dev = self.device if self.rccl else "cpu"
+            g = torch.zeros(2 * self.ndim + 1, dtype=torch.float64, device=dev)
+            tau, exc = None, None
+            try:
+                tau = np.asarray(super().get_autocorr_time(discard=discard, thin=thin, **kwargs), np.float64)
+                t = torch.from_numpy(np.nan_to_num(tau, nan=np.inf)).to(dev)
+                g[: self.ndim] = t
+                g[self.ndim: 2 * self.ndim] = -t
+            except AutocorrError as e:                # emcee's "chain too short": same on every rank
+                g[-1] = 1.0
+                exc = e
+            except Exception as e:
+                g[-1] = 2.0
+                exc = e
+            self.dist.all_reduce(g, op=self.dist.ReduceOp.MAX, group=self.group)
+            flag = float(g[-1])
+            if flag:
+                if exc is not None:
+                    raise exc
+                raise AutocorrError(np.full(self.ndim, np.nan), "autocorrelation estimate failed on another rank")
+            hi, lo = g[: self.ndim].cpu().numpy(), -g[self.ndim: 2 * self.ndim].cpu().numpy()
+            if not np.array_equal(hi, lo):
+                raise RuntimeError(f"ranks disagree on the autocorrelation time (max {hi}, min {lo}): "
+                                   "their chains or FFTs differ")
+            return tau
         src = self.keep_chain
         tau = torch.zeros(self.ndim, dtype=torch.float64, device=self.device if self.rccl else "cpu")
         err = torch.zeros(1, dtype=torch.float64, device=tau.device)

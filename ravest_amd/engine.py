@@ -128,12 +128,14 @@ class RVEngine:
         built on it: "auto" (default), "pageable", "pinned" or "zerocopy" (include/rvk.h)."""
         _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_HOSTIO, _lib.HOSTIO[mode]))
 
-    def set_lds_poison(self, on: bool) -> None:
+    def set_lds_poison(self, on) -> None:
         """RVK_OPT_LDS_POISON (tests only): the kernels fill their LDS sin/cos table with NaN
         first and the real values ~10 us later, so a read not ordered after the publishing
         barrier yields NaN results (include/rvk.h).  Applies to every kernel launched for this
-        handle, its posteriors and GP objects."""
-        _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_LDS_POISON, int(bool(on))))
+        handle, its posteriors and GP objects.  on = 2: the positive control (the real values
+        are never stored: every kernel the option reaches returns NaN)."""
+        v = 2 if (not isinstance(on, bool) and on == 2) else int(bool(on))
+        _lib.check(_lib.load().rvk_set_option(self._h, _lib.OPT_LDS_POISON, v))
 
     def reserve(self, max_walkers: int) -> None:
         _lib.check(_lib.load().rvk_reserve(self._h, int(max_walkers)))

@@ -73,12 +73,14 @@ def test_gp_bjd_times():
 
 
 def test_gp_config5_shape_and_paths():
-    """Config-5 shape (1 planet + GP, 512 epochs): host path == device path, repeatable,
-    invalid planets -inf, and parity with the fp64 oracle on a sample of walkers."""
+    """Config 5 at its BASELINE size (1 planet + GP, 512 epochs, 4096 walkers: 16 walker
+    generations per CU, every workspace slot reused): host path == device path, repeatable,
+    invalid planets -inf, and parity with the fp64 oracle on walkers from the first, a middle
+    and the last generation."""
     import torch
     from oracle import gp_oracle
     from ravest_amd.synth import make_gp_config
-    ds, th, hy = make_gp_config(1024)
+    ds, th, hy = make_gp_config(4096)
     gp = _gp(ds)
     a = gp.batch(th, hy)
     b = gp.batch(th, hy)
@@ -88,7 +90,7 @@ def test_gp_config5_shape_and_paths():
     gp.device(tt, ht, out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), a, equal_nan=True)
-    idx = np.r_[0:24, np.nonzero(~np.isfinite(a))[0][:8]]
+    idx = np.r_[0:12, 2040:2048, 4084:4096, np.nonzero(~np.isfinite(a))[0][:8]]
     ref = gp_oracle.gp_loglike(ds.time, ds.vel, ds.velerr, ds.inst_idx, 1, 1, 0, ds.t0, th[idx], hy[idx])
     _check(a[idx], ref, "config5", 512)
     assert (~np.isfinite(a)).sum() > 0

@@ -76,6 +76,27 @@ def test_fp64_loglike_vs_oracle(n, np_, ni, par, trend):
     assert np.isfinite(ref).sum() >= 30
 
 
+def test_fp64_config5_full_size():
+    """Config 5 at its BASELINE size in the drop-in's default precision (fp64, 512 epochs, 4096
+    walkers: 16 walker generations per CU through the per-CU workspace): host path == device
+    path, repeatable, and the fp64 oracle on walkers of the first, a middle and the last
+    generation, plus the masked ones."""
+    import torch
+    from ravest_amd.synth import make_gp_config
+    ds, th, hy = make_gp_config(4096)
+    gp = _gp(ds, "fp64")
+    a = gp.batch(th, hy)
+    assert np.array_equal(a, gp.batch(th, hy), equal_nan=True)
+    tt, ht = torch.from_numpy(th).cuda(), torch.from_numpy(hy).cuda()
+    out = torch.empty(len(th), dtype=torch.float64, device="cuda")
+    gp.device(tt, ht, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), a, equal_nan=True)
+    idx = np.r_[0:8, 2044:2052, 4088:4096, np.nonzero(~np.isfinite(a))[0][:6]]
+    _check(a[idx], _oracle(ds, th[idx], hy[idx]), RTOL64, "config 5 fp64, 4096 walkers")
+    assert (~np.isfinite(a)).sum() > 0 and np.isfinite(a).sum() > 0.9 * len(a)
+
+
 def test_fp64_bjd_times():
     """BJD-scale epochs: tau = t_i - t_j is formed in fp64 exactly as the reference forms it."""
     from ravest_amd.synth import make_dataset

@@ -109,3 +109,49 @@ def test_poison_reaches_the_kernel(cfg, W):
         return a.elapsed_time(b) * 1e3 / n
     plain, poisoned = _both(eng, us_per_launch)
     assert poisoned > plain + 5.0, (plain, poisoned)
+
+
+def _nan_control(eng, fn):
+    """Run fn with RVK_OPT_LDS_POISON = 2 (the real table values never stored)."""
+    eng.set_lds_poison(2)
+    try:
+        return fn()
+    finally:
+        eng.set_lds_poison(False)
+
+
+def test_poison_control_reaches_every_kernel_family():
+    """Positive control for the equality tests above: with poison = 2 every table
+    read is NaN, so each kernel family the option must reach -- the device log-posterior (DIRECT
+    kernel), the fused sampler half-step, the posterior predictive, the fp64 and fp32 GP
+    factorisations -- returns NaN where the plain run is finite.  If the flag did not reach one
+    of them, its equality test above would pass without testing anything; this one fails."""
+    from ravest_amd.gp import GPKernel, GPLogLikelihood
+    from ravest_amd.sampler import DeviceEnsembleSampler
+    from ravest_amd.synth import make_config, make_gp_config, make_posterior
+    lpost, x0 = make_posterior(2, n_walkers=1024, device=0)
+    eng = lpost.log_likelihood.engine
+    dp = lpost.device_posterior()
+    plain = dp(x0)
+    ctl = _nan_control(eng, lambda: dp(x0))
+    assert np.isnan(ctl[np.isfinite(plain)]).all(), "device log-posterior (DIRECT kernel)"
+
+    def run():
+        s = DeviceEnsembleSampler(lpost, 1024, seed=3)
+        s.run_mcmc(x0, 4)
+    with pytest.raises(ValueError, match="NaN"):
+        _nan_control(eng, run)                     # the fused half-step's log-probs are NaN
+    ds = make_config(2, n_walkers=512)
+    e2 = _engine(ds)
+    tq = np.linspace(ds.time.min(), ds.time.max(), 300)
+    plain = e2.predict(ds.theta, tq)
+    ctl = _nan_control(e2, lambda: e2.predict(ds.theta, tq))
+    assert np.isfinite(plain).any() and np.isnan(ctl[np.isfinite(plain)]).all(), "posterior predictive"
+    dsg, th, hy = make_gp_config(n_walkers=256)
+    for precision in ("fp64", "fp32+fp64"):
+        gp = GPLogLikelihood(dsg.time, dsg.vel, dsg.velerr, dsg.t0, dsg.instrument, dsg.unique_instruments,
+                             dsg.planet_letters, dsg.parameterisation, GPKernel("Quasiperiodic"), precision=precision)
+        plain = gp.batch(th, hy)
+        ctl = _nan_control(gp.engine, lambda: gp.batch(th, hy))
+        fin = np.isfinite(plain)
+        assert fin.sum() > 0.9 * len(plain) and np.isnan(ctl[fin]).all(), f"GP {precision}"

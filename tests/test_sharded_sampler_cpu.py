@@ -58,12 +58,27 @@ def _worker(rank, world, port, q, mode, storage="auto"):
             s = _sampler(keep=0, storage=storage)
             hist = ravest_convergence_loop(s, _x0(), LOOP_STEPS, 25, 50)
             q.put((rank, s.iteration, s.naccepted.copy(), sorted(hist), s.acceptance_fraction.copy()))
-        elif mode == "tau_all":                            # keep_chain="all": no collective in the estimate
+        elif mode == "tau_all":                            # keep_chain="all": local estimate + guard
             s = _sampler(storage=storage)
             s.run_mcmc(_x0(), 60)
-            tau = s.get_autocorr_time(tol=0) if rank == 1 else None   # one rank only: must not block
-            dist.barrier()
-            q.put((rank, tau, s.get_autocorr_time(tol=0)))
+            short = None
+            try:
+                s.get_autocorr_time()                      # tol=50 on 60 steps: too short on every rank
+            except Exception as e:
+                short = type(e).__name__
+            q.put((rank, short, s.get_autocorr_time(tol=0)))
+        elif mode == "tau_disagree":                       # one rank's estimate differs in the last bit
+            from ravest_amd.distributed import _DevicePipeline
+            s = _sampler(storage=storage)
+            s.run_mcmc(_x0(), 60)
+            if rank == 1:
+                base = _DevicePipeline.get_autocorr_time
+                _DevicePipeline.get_autocorr_time = lambda self, **kw: np.nextafter(base(self, **kw), np.inf)
+            try:
+                s.get_autocorr_time(tol=0)
+                q.put((rank, "no error"))
+            except RuntimeError as e:
+                q.put((rank, str(e)))
         elif mode == "keep":
             s = _sampler(keep=0, storage=storage)
             s.run_mcmc(_x0(), STEPS)
@@ -180,8 +195,16 @@ def test_convergence_loop_with_chain_on_one_rank(storage):
 
 
 def test_autocorr_time_local_with_keep_chain_all():
-    """keep_chain="all": get_autocorr_time is computed locally (a call on one rank alone does not
-    block), and every rank's estimate is the same."""
+    """keep_chain="all": get_autocorr_time is computed on each rank, and one guard all-reduce
+    makes the ranks agree: same estimate everywhere, and a too-short chain raises emcee's
+    AutocorrError on every rank (none is left waiting in a collective)."""
     res = _spawn(2, "tau_all")
-    assert res[0][1] is None and res[1][1] is not None
-    assert np.array_equal(res[0][2], res[1][2]) and np.array_equal(res[1][1], res[1][2])
+    assert all(r[1] == "AutocorrError" for r in res), res
+    assert np.array_equal(res[0][2], res[1][2]) and np.all(np.isfinite(res[0][2]))
+
+
+def test_autocorr_time_disagreement_raises_on_every_rank():
+    """if one rank's estimate differs (another FFT plan, another GPU SKU), every rank
+    raises instead of one leaving ravest's convergence loop while the others hang."""
+    res = _spawn(2, "tau_disagree")
+    assert all("disagree" in r[1] for r in res), res
