@@ -70,6 +70,15 @@ namespace {
 #ifndef RVK_EPOCH_OFF32
 #define RVK_EPOCH_OFF32 1             // epoch loads through one 32-bit byte offset (global_load saddr form)
 #endif
+#ifndef RVK_EPOCH_UNI
+#define RVK_EPOCH_UNI 1               // epoch loop with a wave-uniform trip count over padded epoch arrays (1)
+#endif
+#ifndef RVK_SOLVE_UNI
+#define RVK_SOLVE_UNI 1               // loglike_kernel (one walker per wave): e-dependent solver choices as scalar branches
+#endif
+#ifndef RVK_PAIR_RENORM
+#define RVK_PAIR_RENORM 1             // epoch pairs share one renormalisation of the s^2 product when safe (same bits)
+#endif
 #ifndef RVK_PK_SGPR
 #define RVK_PK_SGPR 2                 // NP >= this: planet constants moved to SGPRs, else left in VGPRs
                                       // (NP = 1 in VGPRs: 34 -> 7 SGPR spills, -2.5 % config 2;
@@ -143,12 +152,22 @@ __device__ __forceinline__ double epoch_sum(const EpochData &d, int n_epochs, in
     const double g0 = g[0], j0 = jit[0] * jit[0];
     double chi2 = 0.0, prod = 0.5;   // prod * 2^expo = running product of s^2
     int expo = 1;
+    KFlags kf[NP > 0 ? NP : 1];      // the solver's per-planet choices, wave-uniform (one walker per wave)
+    if constexpr (RVK_SOLVE_UNI && NP > 0) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) kf[p] = kflags_uniform(pk[p].e);
+    }
     // The epoch loop, versioned on the (wave-uniform) trend so the trend-free
     // common case carries no trend arithmetic at all.
     auto epochs = [&](auto trend_c) {
         constexpr bool TREND = decltype(trend_c)::value;
-        // one epoch: gamma + planets (+ trend), chi^2 term, s^2 into the running product
-        auto one = [&](double t, double vel, double s2b, int ii) {
+        // one epoch: gamma + planets (+ trend), chi^2 term, s^2 into the running product.
+        // PAIR: the first epoch of a pair on the walker-safe path (below): no renormalisation
+        // after it, and no fmin in 1/s^2 (s^2 is finite and normal there, where the fmin is a
+        // no-op): the same bits, since frexp only scales by a power of two.
+        auto one = [&](double t, double vel, double s2b, int ii, auto pair_c) {
+            constexpr int PM = decltype(pair_c)::value;   // 0 single, 1 first of a pair, 2 second
+            constexpr bool PAIR = PM != 0;
             double gam = g0, jj = j0;
             if (MULTI) {
                 for (int k = 1; k < n_inst; ++k) {
@@ -158,7 +177,7 @@ __device__ __forceinline__ double epoch_sum(const EpochData &d, int n_epochs, in
             double rv = gam - vel;   // the residual itself: each planet's K * (...) lands in one FMA
             if constexpr (NP > 0) {
 #pragma unroll
-                for (int p = 0; p < NP; ++p) rv = planet_rv<SOLVER>(pk[p], t, tab, rv);
+                for (int p = 0; p < NP; ++p) rv = planet_rv<SOLVER, RVK_SOLVE_UNI>(pk[p], t, tab, rv, kf[p]);
             } else {
                 for (int p = 0; p < np; ++p) rv = planet_rv<SOLVER>(pks[p], t, tab, rv);
             }
@@ -171,13 +190,24 @@ __device__ __forceinline__ double epoch_sum(const EpochData &d, int n_epochs, in
 #if RVK_CHI_NR2
             chi2 = __builtin_fma(r * r, rcp_nr(s2), chi2);
 #else
-            chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);   // <= 2.2e-15 relative per term
+            if constexpr (PAIR) chi2 = __builtin_fma(r * r, rcp_nr1_finite(s2), chi2);
+            else chi2 = __builtin_fma(r * r, rcp_nr1(s2), chi2);   // <= 2.2e-15 relative per term
 #endif
             prod *= s2;
-            int ex;
-            prod = __builtin_frexp(prod, &ex);
-            expo += ex;
+            if constexpr (PM != 1) {
+                int ex;
+                prod = __builtin_frexp(prod, &ex);
+                expo += ex;
+            }
         };
+        const auto single = std::integral_constant<int, 0>{};
+        const auto first = std::integral_constant<int, 1>{};
+        const auto second = std::integral_constant<int, 2>{};
+        // pairs of epochs may share one renormalisation when every s^2 of this walker lies in
+        // [2^-500, 2^501]: then prod in [0.5, 1) times two of them stays a normal number
+        // (no overflow, underflow or denormal), so skipping the power-of-two scaling in
+        // between changes no bit.  Wave-uniform (the data's flag and the walker's jitter).
+        const bool pairsafe = !MULTI && RVK_PAIR_RENORM && d.s2ok && (j0 <= 0x1p500);
         // Lane epochs i, i+64, ...  RVK_UNROLL2: two per trip with ping-pong registers
         // (A, B), no register shuffling between trips; invariant: A holds epoch i.
 #if RVK_UNROLL2
@@ -187,14 +217,64 @@ __device__ __forceinline__ double epoch_sum(const EpochData &d, int n_epochs, in
         for (; i + 64 < n_epochs; i += 128) {
             tB = d.t[i + 64]; vB = d.vel[i + 64]; sB = d.s2[i + 64];
             if (MULTI) iB = d.inst[i + 64];
-            one(tA, vA, sA, iA);
+            one(tA, vA, sA, iA, single);
             if (i + 128 < n_epochs) {
                 tA = d.t[i + 128]; vA = d.vel[i + 128]; sA = d.s2[i + 128];
                 if (MULTI) iA = d.inst[i + 128];
             }
-            one(tB, vB, sB, iB);
+            one(tB, vB, sB, iB, single);
         }
-        if (i < n_epochs) one(tA, vA, sA, iA);
+        if (i < n_epochs) one(tA, vA, sA, iA, single);
+#elif RVK_EPOCH_UNI
+        // Every lane runs `full` = n / 64 trips whose epoch exists, then lanes < n % 64 one more:
+        // the trip count is wave-uniform, so the loop runs on a scalar counter -- no per-lane
+        // compare, exec-mask update or address increment per epoch.  The prefetch of epoch i + 64
+        // is unconditional: the epoch arrays are one padded block (rvk_create: t | vel | s2 | inst,
+        // kEpochPad entries after each), so it reads padding past the end, never out of bounds.
+        // All four arrays are read through ONE buffer descriptor based at t: the lane's offset
+        // (8 lane, 4 lane) is the VGPR operand, the array and the trip are the scalar offset, so
+        // addressing costs no VALU.  One planet: two epochs per trip with ping-pong registers (A
+        // holds the trip's first epoch: no register copies between trips).  Same epochs in the
+        // same order per lane as the other forms: bitwise the same results.
+        const int full = n_epochs >> 6;
+        const bool tail = lane < (n_epochs & 63);
+        const char *b0 = reinterpret_cast<const char *>(d.t);
+        const int ov = (int)(reinterpret_cast<const char *>(d.vel) - b0);
+        const int os = (int)(reinterpret_cast<const char *>(d.s2) - b0);
+        const int oi = (int)(reinterpret_cast<const char *>(d.inst) - b0);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(b0), 0, oi + 4 * (n_epochs + kEpochPad), 0x00020000);
+        const int lo = 8 * lane, li = 4 * lane;
+        auto ldd = [&](int voff, int soff) -> double {
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+        };
+        auto ldi = [&](int soff) -> int { return (int)__builtin_amdgcn_raw_buffer_load_b32(rs, li, soff, 0); };
+        double tA = t_1, vA = v_1, sA = s_1, tB, vB, sB;
+        int iA = i_1, iB = 0;
+        int k = 0;
+        if constexpr (NP == 1) {
+            auto pairs = [&](auto m1, auto m2) {
+                for (; k + 2 <= full; k += 2) {
+                    const int e1 = 512 * (k + 1), e2 = 512 * (k + 2);   // byte offsets of epochs k+1, k+2
+                    tB = ldd(lo, e1); vB = ldd(lo, ov + e1); sB = ldd(lo, os + e1);
+                    if (MULTI) iB = ldi(oi + (e1 >> 1));
+                    one(tA, vA, sA, iA, m1);
+                    tA = ldd(lo, e2); vA = ldd(lo, ov + e2); sA = ldd(lo, os + e2);
+                    if (MULTI) iA = ldi(oi + (e2 >> 1));
+                    one(tB, vB, sB, iB, m2);
+                }
+            };
+            if (pairsafe) pairs(first, second);
+            else pairs(single, single);
+        }
+        for (; k < full; ++k) {            // one trip (NP != 1), or the odd last full trip (NP == 1)
+            const int e1 = 512 * (k + 1);
+            tB = ldd(lo, e1); vB = ldd(lo, ov + e1); sB = ldd(lo, os + e1);
+            if (MULTI) iB = ldi(oi + (e1 >> 1));
+            one(tA, vA, sA, iA, single);
+            tA = tB; vA = vB; sA = sB; iA = iB;
+        }
+        if (tail) one(tA, vA, sA, iA, single);
 #elif RVK_EPOCH_OFF32
         // one epoch per trip; the next epoch's loads are issued before this one's solve.
         // off = 8 (i + 64), the next epoch's byte offset, is the only induction variable:
@@ -209,7 +289,7 @@ __device__ __forceinline__ double epoch_sum(const EpochData &d, int n_epochs, in
                 tn = ld_off(d.t, off); vn = ld_off(d.vel, off); sn = ld_off(d.s2, off);
                 if (MULTI) in_ = ld_off(d.inst, off >> 1);
             }
-            one(t, vel, s2b, ii);
+            one(t, vel, s2b, ii, single);
         }
 #else
         // one epoch per trip; the next epoch's loads are issued before this one's solve
@@ -222,7 +302,7 @@ __device__ __forceinline__ double epoch_sum(const EpochData &d, int n_epochs, in
                 tn = d.t[i + 64]; vn = d.vel[i + 64]; sn = d.s2[i + 64];
                 if (MULTI) in_ = d.inst[i + 64];
             }
-            one(t, vel, s2b, ii);
+            one(t, vel, s2b, ii, single);
         }
 #endif
     };
@@ -1262,11 +1342,8 @@ static int grow(double **p, size_t *cap, size_t need) { return grow_dev((void **
 static void free_handle(rvk_handle *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    (void)hipFree(h->d_t);
+    (void)hipFree(h->d_t);       // one block: t | vel | s2 | inst (rvk_create)
     (void)hipFree(h->d_tab);
-    (void)hipFree(h->d_vel);
-    (void)hipFree(h->d_s2);
-    (void)hipFree(h->d_inst);
     (void)hipFree(h->d_theta);
     (void)hipFree(h->d_out);
     (void)hipFree(h->d_tq);
@@ -1324,17 +1401,33 @@ static int create_impl(rvk_handle *h, const double *time, const double *vel, con
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     if ((rc = upload_table(&h->d_tab))) return rc;
     if (n == 0) return RVK_OK;                                      // model-only handle
-    std::vector<double> s2(n);
-    for (int i = 0; i < n; ++i) s2[i] = velerr[i] * velerr[i];     // velerr ** 2 (fit.py:3598)
-    size_t bd = sizeof(double) * (size_t)n;
-    HIPCHK(hipMalloc(&h->d_t, bd));
-    HIPCHK(hipMalloc(&h->d_vel, bd));
-    HIPCHK(hipMalloc(&h->d_s2, bd));
-    HIPCHK(hipMalloc(&h->d_inst, sizeof(int32_t) * (size_t)n));
-    HIPCHK(hipMemcpy(h->d_t, time, bd, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(h->d_vel, vel, bd, hipMemcpyHostToDevice));
+    // The epoch arrays carry kEpochPad entries of padding (finite values no result reads), so the
+    // likelihood kernel's prefetch of epoch i + 64 is in bounds for every lane without a per-lane
+    // guard (epoch_sum, RVK_EPOCH_UNI).
+    const size_t np_ = (size_t)n + kEpochPad;
+    std::vector<double> s2(np_, 1.0), tp(np_, time[n - 1]), vp(np_, 0.0);
+    std::vector<int32_t> ip(np_, 0);
+    h->s2ok = 1;
+    for (int i = 0; i < n; ++i) {
+        s2[i] = velerr[i] * velerr[i];                              // velerr ** 2 (fit.py:3598)
+        if (!(s2[i] >= 0x1p-500 && s2[i] <= 0x1p500)) h->s2ok = 0;
+        tp[i] = time[i];
+        vp[i] = vel[i];
+        ip[i] = inst[i];
+    }
+    // One allocation, t | vel | s2 | inst (each padded): the likelihood kernel addresses all four
+    // through one buffer descriptor based at t (epoch_sum, RVK_EPOCH_UNI).
+    const size_t bd = sizeof(double) * np_;
+    char *blk = nullptr;
+    HIPCHK(hipMalloc(&blk, 3 * bd + sizeof(int32_t) * np_));
+    h->d_t = reinterpret_cast<double *>(blk);
+    h->d_vel = reinterpret_cast<double *>(blk + bd);
+    h->d_s2 = reinterpret_cast<double *>(blk + 2 * bd);
+    h->d_inst = reinterpret_cast<int32_t *>(blk + 3 * bd);
+    HIPCHK(hipMemcpy(h->d_t, tp.data(), bd, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_vel, vp.data(), bd, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_s2, s2.data(), bd, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(h->d_inst, inst.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_inst, ip.data(), sizeof(int32_t) * np_, hipMemcpyHostToDevice));
     return RVK_OK;
 }
 

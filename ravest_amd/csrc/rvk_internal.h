@@ -17,6 +17,7 @@ namespace rvk {
 
 constexpr int kBlock = 256;                    // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kEpochPad = 64;                  // padding entries after the device epoch arrays (rvk_create)
 
 // Per-epoch data: SoA, device-resident for the handle's lifetime.
 struct EpochData {
@@ -30,6 +31,7 @@ struct EpochData {
     int lpw;              // lanes per walker: 0 = chosen per launch, else 64 / 32 / 16 (RVK_OPT_LPW)
     int np;               // planets (the generic kernels' runtime count; the others are specialised)
     int poison;           // RVK_OPT_LDS_POISON: tab_put writes NaN first (tests only)
+    int s2ok;             // every velerr^2 in [2^-500, 2^500] (rvk_create): epoch_sum may renormalise less often
 };
 
 // Store entry i of an LDS copy of the sin/cos table.  poison (RVK_OPT_LDS_POISON, tests only):
@@ -175,11 +177,12 @@ struct rvk_handle {
     int lpw = 0;                             // RVK_OPT_LPW
     int hostio = RVK_HOSTIO_AUTO;            // RVK_OPT_HOSTIO, shared by the posteriors built on the handle
     int poison = 0;                          // RVK_OPT_LDS_POISON
+    int s2ok = 0;                            // EpochData::s2ok
     rvk::HostIO io;                          // rvk_loglike's transport
     // Held by every blocking (host-buffer) entry point of this handle and of the posteriors /
     // GP objects built on it: they share the handle's stream and staging (include/rvk.h).
     std::mutex mu;
 
-    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw, n_planets, poison}; }
+    rvk::EpochData epochs() const { return rvk::EpochData{d_t, d_vel, d_s2, d_inst, d_tab, t0, par, lpw, n_planets, poison, s2ok}; }
     int p_full() const { return 5 * n_planets + 2 * n_inst + 2; }
 };

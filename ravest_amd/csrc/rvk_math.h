@@ -116,6 +116,13 @@ __device__ __forceinline__ double rcp_nr1(double b) {
     return __builtin_fma(r, __builtin_fmin(__builtin_fma(-b, r, 1.0), 1.0), r);
 }
 
+// rcp_nr1 for a finite positive normal b, where its fmin is a no-op (1 - b r is tiny): the
+// same bits without it.
+__device__ __forceinline__ double rcp_nr1_finite(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+}
+
 // 1/b to ~1 ulp: v_rcp_f64 + two Newton-Raphson steps (finite, normal b).
 __device__ __forceinline__ double rcp_nr(double b) {
     double r = __builtin_amdgcn_rcp(b);
@@ -264,9 +271,23 @@ __device__ __forceinline__ float seed_series(float rf, float ef) {
     return __builtin_fmaf(s, ef * q, rf);
 }
 
+// The solver's e-dependent choices for one planet when e is the same in every lane of the wave
+// (one walker per wave): made once per walker, before the epoch loop, as wave-uniform bools
+// (readfirstlane: scalar branches in the loop, not per-lane masks re-materialised every solve).
+struct KFlags {
+    bool series, precise, le09, le05;
+};
+__device__ __forceinline__ KFlags kflags_uniform(double e) {
+    const float ef = (float)e;
+    auto uni = [](bool b) -> bool { return __builtin_amdgcn_readfirstlane((int)b) != 0; };
+    return KFlags{uni(ef <= RVK_SERIES_E), uni(ef > 0.95f), uni(e <= 0.9), uni(e <= 0.5)};
+}
+
 // r = the mean anomaly reduced to [-pi, pi]; e6e3 = 6*e^3 (per planet, precomputed).
+// UNI: the choices come from kf (kflags_uniform of this e), else they are made per lane.
+template <bool UNI = false>
 __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e6e3, const SC *tab, double &cosE,
-                                                    double &sinE) {
+                                                    double &sinE, KFlags kf = {}) {
     const float rf = (float)r, ef = (float)e;
 #ifndef RVK_SEED_HW
 #define RVK_SEED_HW 1
@@ -274,10 +295,11 @@ __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e
 #ifndef RVK_ABLATE
 #define RVK_ABLATE 0   // timing experiments only (wrong results): 1 = no fp64 stage, 2 = no fp32 seed, 3 = neither
 #endif
-    const bool series = ef <= RVK_SERIES_E;
+    const bool series = UNI ? kf.series : ef <= RVK_SERIES_E;
     const float Ef = (RVK_ABLATE & 2) ? rf
                    : series ? seed_series(rf, ef)
-                   : ((!RVK_SEED_HW || ef > 0.95f) ? seed_f32<true>(rf, ef) : seed_f32<false>(rf, ef));
+                   : ((!RVK_SEED_HW || (UNI ? kf.precise : ef > 0.95f)) ? seed_f32<true>(rf, ef)
+                                                                         : seed_f32<false>(rf, ef));
     double E = (double)Ef, S, C;
     sincos_tab(E, tab, S, C);
     if (RVK_ABLATE & 1) { cosE = C; sinE = S; return; }
@@ -324,18 +346,32 @@ __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e
     };
     // next error ~ (e/f1)^3 d^4.  For e <= 0.9, (e/f1)^3 <= 729, so |d| <= 1e-5 already
     // bounds it by 7.3e-18 (one compare); otherwise estimate it as 6 e^3 d^4 / den.
+    const bool e_le_09 = UNI ? kf.le09 : e <= 0.9;
     auto converged = [&](double d, double t) -> bool {
-        if (RVK_HH_SINGLE && e <= 0.9) return __builtin_fabs(d) <= 1e-5;
+        if (RVK_HH_SINGLE && e_le_09) return __builtin_fabs(d) <= 1e-5;
         const double z2 = (d * d) * (d * d);
         return z2 * e6e3 * __builtin_fabs(t) < 1e-17;
     };
     // The first step is peeled (no loop-carried register shuffles on the common one-step path).
     // Halley's next error is c d^3 with |c| = |f2^2 / (4 f1^2) - f3 / (6 f1)| <= 0.42 for
     // e <= 0.5 (f1 >= 1/2, |f2|, |f3| <= 1/2): |d| <= 2.8e-6 bounds it by 9.2e-18.
-    const bool hal = RVK_HALLEY_LOWE && e <= 0.5;
+    const bool hal = RVK_HALLEY_LOWE && (UNI ? kf.le05 : e <= 0.5);
     double t;
     double d = step(hal, t);
-    const bool done = hal ? __builtin_fabs(d) <= 2.8e-6 : series ? __builtin_fabs(d) <= 1.7e-4 : converged(d, t);
+    bool done;
+    if constexpr (UNI) {
+        // one compare against a wave-uniform threshold (no select between per-lane bools, which
+        // the compiler lowers through a VGPR and back every solve); the same tests as below
+        if (hal) {
+            done = __builtin_fabs(d) <= 2.8e-6;
+        } else if (series || (RVK_HH_SINGLE && e_le_09)) {
+            done = __builtin_fabs(d) <= (series ? 1.7e-4 : 1e-5);
+        } else {
+            done = converged(d, t);
+        }
+    } else {
+        done = hal ? __builtin_fabs(d) <= 2.8e-6 : series ? __builtin_fabs(d) <= 1.7e-4 : converged(d, t);
+    }
     if (!done) {
 #pragma unroll 1
         for (int it = 1; it < 8; ++it) {
@@ -347,9 +383,10 @@ __device__ __forceinline__ void solve_kepler_fast_r(double r, double e, double e
     sinE = S;
 }
 
+template <bool UNI = false>
 __device__ __forceinline__ void solve_kepler_fast(double M, double e, double e6e3, const SC *tab, double &cosE,
-                                                  double &sinE) {
-    solve_kepler_fast_r(reduce_2pi(M), e, e6e3, tab, cosE, sinE);
+                                                  double &sinE, KFlags kf = {}) {
+    solve_kepler_fast_r<UNI>(reduce_2pi(M), e, e6e3, tab, cosE, sinE, kf);
 }
 
 // ---- register-light atan / atan2 / tan for the Tc and secosw/sesinw conversions ----
@@ -506,10 +543,10 @@ __device__ __attribute__((noinline)) bool planet_consts_lds(int par, const doubl
 
 // One planet's RV at time t (model.py:327, 119-121, 170).  e == 0 takes the
 // same arithmetic (the solvers return E = M), so there is no branch.
-template <int SOLVER>
-// acc + (this planet's RV at t).  1/(1 - e cos E) with one Newton step on v_rcp_f64
+template <int SOLVER, bool UNI = false>
+// acc + (this planet's RV at t).  UNI: pk is the same in every lane (solve_kepler_fast_r).  1/(1 - e cos E) with one Newton step on v_rcp_f64
 // (<= 2.2e-15 relative, like the chi^2 terms); the divisor is in (0, 2).
-__device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const SC *tab, double acc) {
+__device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const SC *tab, double acc, KFlags kf = {}) {
     double cE, sE;
     if (SOLVER == 1) {
         const double M = RVK_PHASE ? kTwoPi * (pk.n * (t - pk.Tp)) : pk.n * (t - pk.Tp);
@@ -521,9 +558,9 @@ __device__ __forceinline__ double planet_rv(const PlanetK &pk, double t, const S
         // product into the subtraction would leave its rounding error, ~ulp(u), in the fraction.
 #pragma clang fp contract(off)
         const double u = pk.n * (t - pk.Tp);
-        solve_kepler_fast_r(kTwoPi * (u - __builtin_rint(u)), pk.e, pk.e6e3, tab, cE, sE);
+        solve_kepler_fast_r<UNI>(kTwoPi * (u - __builtin_rint(u)), pk.e, pk.e6e3, tab, cE, sE, kf);
     } else {
-        solve_kepler_fast(pk.n * (t - pk.Tp), pk.e, pk.e6e3, tab, cE, sE);
+        solve_kepler_fast<UNI>(pk.n * (t - pk.Tp), pk.e, pk.e6e3, tab, cE, sE, kf);
     }
     const double b = 1.0 - pk.e * cE;
     double inv = __builtin_amdgcn_rcp(b);
