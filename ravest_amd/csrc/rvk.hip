@@ -71,13 +71,19 @@ namespace {
 #define RVK_EPOCH_OFF32 1             // epoch loads through one 32-bit byte offset (global_load saddr form)
 #endif
 #ifndef RVK_EPOCH_UNI
-#define RVK_EPOCH_UNI 1               // epoch loop with a wave-uniform trip count over padded epoch arrays (1)
+// epoch loop with a wave-uniform trip count over the padded epoch block (1); the fused half-step
+// units keep the per-lane loop (sessions sa1/sa2, tools/sampler_ab.sh: 16.5-16.7 vs 17.0 us per
+// config-2 sampler step; the plain likelihood kernels take the uniform loop)
+#define RVK_EPOCH_UNI (RVK_TU_SAMPLE == 0)
 #endif
 #ifndef RVK_SOLVE_UNI
 #define RVK_SOLVE_UNI 1               // loglike_kernel (one walker per wave): e-dependent solver choices as scalar branches
 #endif
 #ifndef RVK_PAIR_RENORM
 #define RVK_PAIR_RENORM 1             // epoch pairs share one renormalisation of the s^2 product when safe (same bits)
+#endif
+#ifndef RVK_DRAW_VMEM
+#define RVK_DRAW_VMEM 0               // fused half-step: the draw and state pointers by vector (1) or scalar (0) loads
 #endif
 #ifndef RVK_PK_SGPR
 #define RVK_PK_SGPR 2                 // NP >= this: planet constants moved to SGPRs, else left in VGPRs
@@ -430,15 +436,32 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         }
         const long long j = sa.j0 + w;   // global proposal index within the half
         const PreDraw *pp = sa.pre + ((long long)sa.step * 2 + sa.half) * sa.hfull + j;
+        using gdp = const __attribute__((address_space(1))) double *;   // global loads (a flat one holds lgkmcnt)
+#if RVK_DRAW_VMEM
+        // the draw and the state pointers through the vector memory path (a VGPR offset makes
+        // them vector loads), not the scalar cache
+        int zo = 0;
+        asm volatile("" : "+v"(zo));
+        using gll = const __attribute__((address_space(1))) long long *;
+        const gll pw = (gll)(reinterpret_cast<const char *>(pp) + zo);
+        const gll rw = (gll)(reinterpret_cast<const char *>(sa.run) + zo);
+        const long long ps = pw[3], pc = pw[4];
+        const double pz = __builtin_bit_cast(double, pw[0]), pfac = __builtin_bit_cast(double, pw[1]),
+                     plau = __builtin_bit_cast(double, pw[2]);
+        const gdp rx = (gdp)rw[offsetof(RunArgs, x) / 8];
+        const gdp rlp = (gdp)rw[offsetof(RunArgs, lp) / 8];
+        const __attribute__((address_space(1))) long long *const rnacc =
+            (const __attribute__((address_space(1))) long long *)rw[offsetof(RunArgs, nacc) / 8];
+#else
         // every scalar load of the fetch (the draw, the state pointers) issued before any is used:
         // one wait for all of them instead of a wait per load
         const long long ps = pp->s, pc = pp->c;
         const double pz = pp->z, pfac = pp->fac, plau = pp->lau;
-        using gdp = const __attribute__((address_space(1))) double *;   // global loads (a flat one holds lgkmcnt)
         const gdp rx = (gdp)sa.run->x;
         const gdp rlp = (gdp)sa.run->lp;
         const __attribute__((address_space(1))) long long *const rnacc =
             (const __attribute__((address_space(1))) long long *)sa.run->nacc;
+#endif
         if (RVK_FUSE_PROLOGUE) __builtin_amdgcn_sched_barrier(0);
         f.s = ps;
         f.c = pc;
@@ -1162,6 +1185,12 @@ sample_launch_t pick_sample(int np, bool multi, bool tp) {
 // the others ~1 % slower; the plain likelihood kernels lose 1-3.5 % under either (tools/kbench.py),
 // so they keep the default scheduler in rvk.hip.
 #if RVK_TU_SAMPLE == 2
+#if RVK_LL_TRACE
+// the phase stamps of THIS build's kernels (each translation unit has its own g_ll_trace)
+extern "C" int rvk_ll_trace_dump_s1(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ll_trace), sizeof(g_ll_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 rvk::sample_launch_t rvk::pick_sample_fused_np1(int mode, bool multi, bool tp) {
     switch (mode) {
         case 2: return pick_sample<2>(1, multi, tp);

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Build librvk_lltrace.so with -DRVK_LL_TRACE=1 on rvk.hip (reuses rvk_post.o, rvk_gp.o).
+# Build the phase-trace library varlib/trace/librvk_lltrace.so (-DRVK_LL_TRACE=1) from the working tree:
+# the likelihood unit (rvk.hip) and the config-2 sampler unit (rvk_sample1.hip) with the stamps, the
+# other units from the in-tree build (make first).  tools/ll_trace.py / tools/sampler_trace.py read it.
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p build/variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -DRVK_LL_TRACE=1 -c -o build/variants/rvk_lltrace.o ravest_amd/csrc/rvk.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/variants/librvk_lltrace.so build/variants/rvk_lltrace.o build/obj/rvk_post.o build/obj/rvk_gp.o build/obj/rvk_gp64.o
+TUS="rvk rvk_sample1" VAROUT=varlib/trace bash tools/varbuild.sh lltrace:"-DRVK_LL_TRACE=1"

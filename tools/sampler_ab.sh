@@ -1,17 +1,35 @@
 #!/bin/bash
-# Sampler: GPU tests (device sampler parity), then bench.py's device stretch-move line (HIP events), base vs variants.
-O=gpurun_out/${1:-samp}
+# Fused half-step A/B: sampler_variants on the in-tree library and varlib/librvk_*.so (REPS interleaved),
+# then the phase trace of every varlib/trace/librvk_lltrace*.so.   bash tools/sampler_ab.sh TAG [REPS] [posteriors]
+TAG=${1:?tag}; REPS=${2:-3}; shift 2; POST=${@:-uniform beta vaneylen}
+O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_sampling.py tests/test_gpu_device_posterior.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
-B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-gp --no-predictive --no-configs"
-ext() { python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(d['sampler']['ms_per_step']*1e3,2), 'us/step')" $1; }
-for rep in 1 2 3; do
-  timeout -k 10 120 $B > $O/base_$rep.json 2>/dev/null || { echo fail; exit 1; }
-  echo "base $(ext $O/base_$rep.json)"
-  for so in build/variants/librvk_*.so; do
+export TMPDIR=/tmp
+for rep in $(seq 1 $REPS); do
+  timeout -k 10 200 python tools/sampler_variants.py $POST > $O/sv_main_$rep.log 2>&1 || { tail -20 $O/sv_main_$rep.log; exit 1; }
+  for so in $(ls varlib/librvk_*.so 2>/dev/null); do
     v=$(basename $so .so)
-    RAVEST_AMD_LIB=$so timeout -k 10 120 $B > $O/${v}_$rep.json 2>/dev/null || { echo fail $v; exit 1; }
-    echo "$v $(ext $O/${v}_$rep.json)"
+    RAVEST_AMD_LIB=$so timeout -k 10 200 python tools/sampler_variants.py $POST > $O/sv_${v}_$rep.log 2>&1 || { tail -20 $O/sv_${v}_$rep.log; exit 1; }
   done
 done
+for so in $(ls varlib/trace/librvk_lltrace*.so 2>/dev/null); do
+  v=$(basename $so .so)
+  RAVEST_AMD_LIB=$so timeout -k 10 120 python tools/sampler_trace.py > $O/trace_$v.txt 2>&1 || { tail -20 $O/trace_$v.txt; exit 1; }
+done
+python - $O <<'PY'
+import json, glob, sys, collections
+o = sys.argv[1]
+res = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in sorted(glob.glob(o + "/sv_*_*.log")):
+    lib = f.split("/sv_")[1].rsplit("_", 1)[0]
+    for line in open(f):
+        try:
+            d = json.loads(line)
+        except Exception:
+            continue
+        for k, v in d.items():
+            res[k][lib].append(round(v["ms_per_step"] * 1e3, 2))
+for k, libs in res.items():
+    print(k, dict(libs))
+PY
+echo "sampler_ab: done"

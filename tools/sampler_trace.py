@@ -1,5 +1,5 @@
 """Per-phase trace of the fused stretch-move half-step (loglike_kernel SAMPLE == 2) on the config-2
-posterior (build with tools/ll_trace.sh: -DRVK_LL_TRACE=1).  For sampled blocks x 4 waves of the
+posterior (build: TUS=rvk_sample1 VAROUT=varlib/trace tools/varbuild.sh lltrace:-DRVK_LL_TRACE=1).  For sampled blocks x 4 waves of the
 last launch: s_memrealtime at entry/exit (100 MHz) and s_memtime (shader cycles) after the
 preload, the prep (proposal + planet constants), the barrier, the epoch loop, the reduction."""
 import ctypes as C, os, sys
@@ -18,7 +18,9 @@ def main():
     s.run_mcmc(x0, 16)
     torch.cuda.synchronize()
     buf = np.zeros((16, 8), dtype=np.uint64)
-    assert _lib.load().rvk_ll_trace_dump(buf.ctypes.data_as(C.c_void_p)) == 0
+    L = _lib.load()
+    dump = getattr(L, "rvk_ll_trace_dump_s1", None) or L.rvk_ll_trace_dump   # the sampler unit's stamps
+    assert dump(buf.ctypes.data_as(C.c_void_p)) == 0
     r0 = buf[:12, 0].astype(np.int64).min()
     print("wave  start_ns  end_ns | cycles: preload->pass  prep  epochs  reduce+epilogue")
     for i in range(12):
