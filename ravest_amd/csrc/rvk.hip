@@ -82,9 +82,6 @@ namespace {
 #ifndef RVK_PAIR_RENORM
 #define RVK_PAIR_RENORM 1             // epoch pairs share one renormalisation of the s^2 product when safe (same bits)
 #endif
-#ifndef RVK_DRAW_VMEM
-#define RVK_DRAW_VMEM 0               // fused half-step: the draw and state pointers by vector (1) or scalar (0) loads
-#endif
 #ifndef RVK_PK_SGPR
 #define RVK_PK_SGPR 2                 // NP >= this: planet constants moved to SGPRs, else left in VGPRs
                                       // (NP = 1 in VGPRs: 34 -> 7 SGPR spills, -2.5 % config 2;
@@ -437,22 +434,6 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const long long j = sa.j0 + w;   // global proposal index within the half
         const PreDraw *pp = sa.pre + ((long long)sa.step * 2 + sa.half) * sa.hfull + j;
         using gdp = const __attribute__((address_space(1))) double *;   // global loads (a flat one holds lgkmcnt)
-#if RVK_DRAW_VMEM
-        // the draw and the state pointers through the vector memory path (a VGPR offset makes
-        // them vector loads), not the scalar cache
-        int zo = 0;
-        asm volatile("" : "+v"(zo));
-        using gll = const __attribute__((address_space(1))) long long *;
-        const gll pw = (gll)(reinterpret_cast<const char *>(pp) + zo);
-        const gll rw = (gll)(reinterpret_cast<const char *>(sa.run) + zo);
-        const long long ps = pw[3], pc = pw[4];
-        const double pz = __builtin_bit_cast(double, pw[0]), pfac = __builtin_bit_cast(double, pw[1]),
-                     plau = __builtin_bit_cast(double, pw[2]);
-        const gdp rx = (gdp)rw[offsetof(RunArgs, x) / 8];
-        const gdp rlp = (gdp)rw[offsetof(RunArgs, lp) / 8];
-        const __attribute__((address_space(1))) long long *const rnacc =
-            (const __attribute__((address_space(1))) long long *)rw[offsetof(RunArgs, nacc) / 8];
-#else
         // every scalar load of the fetch (the draw, the state pointers) issued before any is used:
         // one wait for all of them instead of a wait per load
         const long long ps = pp->s, pc = pp->c;
@@ -461,7 +442,6 @@ __global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) v
         const gdp rlp = (gdp)sa.run->lp;
         const __attribute__((address_space(1))) long long *const rnacc =
             (const __attribute__((address_space(1))) long long *)sa.run->nacc;
-#endif
         if (RVK_FUSE_PROLOGUE) __builtin_amdgcn_sched_barrier(0);
         f.s = ps;
         f.c = pc;
