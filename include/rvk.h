@@ -167,7 +167,8 @@ const char *rvk_last_error(void);
 /* 100*major + minor.  101: rvk_stretch_run / rvk_gp_stretch_run take an int32 flags
  * argument after step0 and rvk_stretch_half is gone (a caller built against 100 must
  * not call them); RVK_OPT_HOSTIO added.  102: RVK_OPT_LDS_POISON; the blocking calls
- * are serialised per handle (Threading, above). */
+ * are serialised per handle (Threading, above).  103: RVK_OPT_LDS_POISON value 2 (the
+ * tests' positive control). */
 int rvk_version(void);
 
 #ifdef __cplusplus

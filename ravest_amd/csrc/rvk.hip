@@ -1336,7 +1336,7 @@ int rvk_ll_trace_dump(unsigned long long *host) {
 }
 #endif
 
-int rvk_version(void) { return 102; }
+int rvk_version(void) { return 103; }
 
 const char *rvk_last_error(void) { return g_err.c_str(); }
 

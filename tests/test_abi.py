@@ -33,7 +33,7 @@ def test_version_and_errors_without_gpu():
     import torch
     from ravest_amd import _lib
     L = _lib.load()
-    assert L.rvk_version() == 102          # 102: RVK_OPT_LDS_POISON, blocking calls serialised per handle
+    assert L.rvk_version() == 103          # 103: RVK_OPT_LDS_POISON value 2 (positive control)
     if torch.cuda.is_available():
         pytest.skip("this checks the no-device error path")
     t = np.linspace(0, 10, 8)
