@@ -436,12 +436,26 @@ class _SamplerBase:
             raise ValueError("The initial log_prob was NaN")
 
     @staticmethod
-    def _unsupported(thin_by, thin, blobs0) -> None:
-        if thin is not None or thin_by != 1:
-            raise NotImplementedError("the device samplers store every step (thinned storage, thin_by / thin, "
-                                      "is the host EnsembleSampler's); thin at read time with get_chain(thin=...)")
+    def _unsupported(blobs0) -> None:
         if blobs0 is not None:
             raise NotImplementedError("blobs are not supported (ravest's log-probabilities have none)")
+
+    @staticmethod
+    def _thinning(iterations, thin_by, thin):
+        """emcee 3.1's thinning arguments -> (raw steps per yielded step, raw steps per stored step,
+        rows stored): ``thin_by=k`` runs k steps per yielded step and stores every k-th; the
+        deprecated ``thin=k`` yields every step and stores every k-th (iterations // k rows)."""
+        if thin is not None:
+            import warnings
+            warnings.warn("The 'thin' argument is deprecated. Use 'thin_by' instead.", DeprecationWarning)
+            thin = int(thin)
+            if thin <= 0:
+                raise ValueError("Invalid thinning argument")
+            return 1, thin, int(iterations) // thin
+        thin_by = int(thin_by)
+        if thin_by <= 0:
+            raise ValueError("Invalid thinning argument")
+        return thin_by, thin_by, int(iterations)
 
     def run_mcmc(self, initial_state, nsteps: int, **kwargs):
         """emcee: iterate sample() for nsteps steps; returns the last State."""
@@ -753,8 +767,56 @@ class _DevicePipeline(_SamplerBase):
     def sample(self, initial_state=None, log_prob0=None, rstate0=None, blobs0=None, iterations=1, tune=False,
                skip_initial_state_check=False, thin_by=1, thin=None, store=True, progress=False, progress_kwargs=None,
                _per_step=True):
-        """emcee's EnsembleSampler.sample: yields a State per step (``iteration`` counts them)."""
-        self._unsupported(thin_by, thin, blobs0)
+        """emcee's EnsembleSampler.sample: yields a State per step (``iteration`` counts the stored
+        ones).  Thinning as emcee 3.1 (``thin_by=k``: k steps per yielded step, every k-th stored;
+        the deprecated ``thin=k``: every step yielded, every k-th stored), with emcee's accounting:
+        only the stored steps' acceptances count (backend.save_step).  The steps between two stored
+        ones run as unstored device steps (their acceptances go to a scratch counter); a stored step
+        is one device step into the backend's next row.  The draws are keyed by the global step, so
+        a thinned run is the unthinned chain's every k-th row, bit for bit."""
+        self._unsupported(blobs0)
+        if thin is None and int(thin_by) == 1:
+            yield from self._sample_steps(initial_state, log_prob0, rstate0, iterations, skip_initial_state_check,
+                                          store, progress, _per_step)
+            return
+        yield_step, checkpoint, nsaves = self._thinning(iterations, thin_by, thin)
+        total = int(iterations) * yield_step
+        if store and self._keep_host:                # the rows of the whole run at once (not one per save)
+            self._settle()
+            if self._dev_chain and not self._device_chain_fits(nsaves):
+                self._chain_to_host()
+            self.backend.grow(nsaves)
+        start = dict(initial_state=initial_state, log_prob0=log_prob0, rstate0=rstate0,
+                     skip_initial_state_check=skip_initial_state_check)
+        bar = _progress_bar(progress, total)
+        i, last = 0, None
+        while i < total:
+            # raw steps up to the next stored step (checkpoint) or the run's end
+            ck = min((i // checkpoint + 1) * checkpoint, total)
+            stored = store and ck % checkpoint == 0
+            n_plain = ck - i - (1 if stored else 0)
+            for part_store, n in ((False, n_plain), (store, 1 if stored else 0)):
+                if n <= 0:
+                    continue
+                per = _per_step and yield_step == 1          # thin=k yields every raw step
+                for st in self._sample_steps(iterations=n, store=part_store, _per_step=per, **start):
+                    start = {}
+                    last = st
+                    if per:
+                        yield st
+                i += n
+                if bar is not None:
+                    bar.update(n)
+                if not per and _per_step and i % yield_step == 0:
+                    yield last
+        if bar is not None:
+            bar.close()
+        if not _per_step and last is not None:
+            yield last
+
+    def _sample_steps(self, initial_state=None, log_prob0=None, rstate0=None, iterations=1,
+                      skip_initial_state_check=False, store=True, progress=False, _per_step=True):
+        """sample() without thinning: every device step is yielded (and stored when `store`)."""
         self._settle()
         self._token += 1
         tok = self._token

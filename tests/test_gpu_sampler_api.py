@@ -220,3 +220,25 @@ def test_reset_does_not_replay_the_draws():
         pass
     g.run_mcmc(x0, 50)
     assert np.array_equal(g.get_chain(), s.get_chain())
+
+
+@pytest.mark.parametrize("storage", ["device", "host"])
+def test_device_sampler_thin_by(storage):
+    """emcee 3.1's thin_by on the GPU sampler: the stored rows are the unthinned run's every k-th
+    row bit for bit, iteration counts the stored steps, and naccepted only their acceptances (emcee's
+    backend.save_step)."""
+    from ravest_amd.sampler import DeviceEnsembleSampler
+    from ravest_amd.synth import make_posterior
+    lpost, x0 = make_posterior(2, 128, seed=8)
+    k, n = 4, 10
+    ref = DeviceEnsembleSampler(lpost, 128, seed=5, steps_per_call=16)
+    cum = [np.zeros(128, dtype=np.int64)]
+    for _ in ref.sample(x0, iterations=n * k):
+        cum.append(ref.naccepted.copy())
+    acc = np.diff(np.array(cum), axis=0)
+    s = DeviceEnsembleSampler(lpost, 128, seed=5, steps_per_call=16, chain_storage=storage)
+    s.run_mcmc(x0, n, thin_by=k)
+    assert s.iteration == n
+    assert np.array_equal(s.get_chain(), ref.get_chain()[k - 1::k])
+    assert np.array_equal(s.get_log_prob(), ref.get_log_prob()[k - 1::k])
+    assert np.array_equal(s.naccepted, acc[k - 1::k].sum(axis=0)) and s.naccepted.sum() > 0

@@ -208,3 +208,44 @@ def test_autocorr_time_disagreement_raises_on_every_rank():
     raises instead of one leaving ravest's convergence loop while the others hang."""
     res = _spawn(2, "tau_disagree")
     assert all("disagree" in r[1] for r in res), res
+
+
+def _per_step_acceptances(n):
+    """Per-step acceptance vectors of an unthinned run (differences of the cumulative counts)."""
+    r = _sampler()
+    cum = [np.zeros(W, dtype=np.int64)]
+    for _ in r.sample(_x0(), iterations=n):
+        cum.append(r.naccepted.copy())
+    return r, np.diff(np.array(cum), axis=0)
+
+
+@pytest.mark.parametrize("k,storage", [(3, "host"), (4, "device"), (1, "device")])
+def test_device_pipeline_thin_by(k, storage):
+    """emcee 3.1's thin_by on the device pipeline (DeviceEnsembleSampler / ShardedDeviceSampler):
+    k steps per yielded step, every k-th stored -- the unthinned chain's rows k-1, 2k-1, ... bit for
+    bit (the draws are keyed by the global step) -- and emcee's accounting: iteration counts the
+    stored steps, naccepted only their acceptances."""
+    n = 7
+    ref, acc = _per_step_acceptances(n * k)
+    s = _sampler(storage=storage)
+    ys = list(s.sample(_x0(), iterations=n, thin_by=k))
+    assert len(ys) == n and s.iteration == n
+    assert np.array_equal(s.get_chain(), ref.get_chain()[k - 1::k])
+    assert np.array_equal(s.get_log_prob(), ref.get_log_prob()[k - 1::k])
+    assert np.array_equal(s.naccepted, acc[k - 1::k].sum(axis=0))
+    assert np.array_equal(np.asarray(ys[-1].coords), ref.get_chain()[-1])
+    s.run_mcmc(None, 2, thin_by=k)                   # continues: 2 more stored rows
+    assert s.iteration == n + 2
+
+
+def test_device_pipeline_thin_deprecated():
+    """The deprecated thin=k: every step yielded, every k-th stored (iterations // k rows)."""
+    ref, acc = _per_step_acceptances(11)
+    s = _sampler()
+    with pytest.warns(DeprecationWarning):
+        ys = list(s.sample(_x0(), iterations=11, thin=3))
+    assert len(ys) == 11 and s.iteration == 3
+    assert np.array_equal(s.get_chain(), ref.get_chain()[2:9:3])
+    assert np.array_equal(s.naccepted, acc[2:9:3].sum(axis=0))
+    with pytest.raises(ValueError):
+        next(s.sample(None, iterations=2, thin_by=0))
