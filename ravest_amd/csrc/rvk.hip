@@ -94,6 +94,11 @@ namespace {
 #define RVK_LL_BLOCK 1024             // threads per loglike_kernel block for NP = 1 and W >= 256 blocks' worth
                                       // (one wave preps 16 walkers: -7 % "P K e w Tc", +-0 "P K e w Tp")
 #endif
+#ifndef RVK_FUSE_LB
+#define RVK_FUSE_LB 8                 // fused half-step kernels, NP > 1: min waves per SIMD x BLK / kBlock (8: 4 waves, <= 128 VGPRs,
+                                      // two 512-thread blocks per CU; session lb: config 3 257 -> 227-237 us, config 4
+                                      // 347 -> 292-296 us per sampler step, against 130-140 VGPRs at 1 block per CU)
+#endif
 #ifndef RVK_LB_WAVES
 #define RVK_LB_WAVES 1                // min waves/SIMD for loglike_kernel, NP > 1 (NP == 1: 4, <= 128 VGPRs)
 #endif
@@ -352,7 +357,7 @@ struct PassCfg {
 };
 
 template <int NP, bool MULTI, int SOLVER, bool TP, int SAMPLE, int BLK = kBlock>
-__global__ __launch_bounds__(BLK, (NP == 1 ? 4 : RVK_LB_WAVES) * kBlock / BLK) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
+__global__ __launch_bounds__(BLK, ((NP == 1 || (SAMPLE & 3) >= 2) ? (NP == 1 ? 4 : RVK_FUSE_LB) : RVK_LB_WAVES) * kBlock / BLK) void loglike_kernel(EpochData d, int n_epochs, int n_inst,
                                                          const double *__restrict__ theta, long long n_walkers,
                                                          long long stride, int wb, double *__restrict__ out,
                                                          PostArgs post, SampleArgs sa) {
