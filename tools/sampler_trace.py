@@ -22,10 +22,11 @@ def main():
     dump = getattr(L, "rvk_ll_trace_dump_s1", None) or L.rvk_ll_trace_dump   # the sampler unit's stamps
     assert dump(buf.ctypes.data_as(C.c_void_p)) == 0
     r0 = buf[:12, 0].astype(np.int64).min()
-    print("wave  start_ns  end_ns | cycles: preload->pass  prep  epochs  reduce+epilogue")
+    print("wave  start_ns  end_ns | cycles: preload->pass  prep (rows wait / compute)  epochs  reduce+epilogue")
     for i in range(12):
         b = buf[i].astype(np.int64)
-        print(f"{i:3d} {(b[0]-r0)*10:8d} {(b[7]-r0)*10:8d} | {b[3]-b[1]:6d} {b[2]-b[3]:7d} {b[4]-b[2]:7d} {b[5]-b[4]:7d}")
+        rows = f"({b[6]-b[3]:5d} / {b[2]-b[6]:5d})" if b[6] else ""
+        print(f"{i:3d} {(b[0]-r0)*10:8d} {(b[7]-r0)*10:8d} | {b[3]-b[1]:6d} {b[2]-b[3]:7d} {rows} {b[4]-b[2]:7d} {b[5]-b[4]:7d}")
 
 
 if __name__ == "__main__":
