@@ -41,7 +41,7 @@ def main():
     # which SIMD each wave of a workgroup runs on (HW_REG_HW_ID bits 5:4), over all blocks
     hw = np.zeros((1024, 8), dtype=np.uint32)
     lib = _lib.load()
-    if hasattr(lib, "rvk_gp64_hwid_dump") and lib.rvk_gp64_hwid_dump(hw.ctypes.data_as(C.c_void_p)) == 0:
+    if callable(getattr(lib, "rvk_gp64_hwid_dump", None)) and lib.rvk_gp64_hwid_dump(hw.ctypes.data_as(C.c_void_p)) == 0:
         from collections import Counter
         simd = (hw[:256] >> 4) & 3
         pats = Counter(tuple(int(x) for x in r) for r in simd)
