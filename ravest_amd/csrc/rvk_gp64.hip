@@ -343,20 +343,6 @@ __device__ __attribute__((noinline)) FactorAcc factor_diag(lds_d *fb, lds_d *li,
 #ifndef RVK_GP64_RING
 #define RVK_GP64_RING 2   // operand register sets (round 4: 6.24-6.34 ms vs 6.40-6.46 with 3, after the other changes)
 #endif
-// Ring depth of spans of one and of two rows.  A set holds 8 + 8 R registers, so a span of one row
-// can keep 3 quarters in flight (4 sets) in the registers a three-row span uses for 2 sets; a
-// one-row span with 2 sets runs latency-bound (phase trace: ~1.4 k cycles per quarter of 8 MFMAs).
-#ifndef RVK_GP64_RING1
-#define RVK_GP64_RING1 RVK_GP64_RING
-#endif
-#ifndef RVK_GP64_RING2
-#define RVK_GP64_RING2 RVK_GP64_RING
-#endif
-// (The LDS-slot shape only: the 5-row kernels keep their register allocation -- a build of
-// gp64_kernel<8, 5> with these rings, 1040 B of scratch, faulted at n = 700 like round 5's
-// RVK_GP64_FLOW build)
-template <int MAXR, int R, int D>
-constexpr int ring_for() { return MAXR != 3 ? D : R == 1 ? RVK_GP64_RING1 : R == 2 ? RVK_GP64_RING2 : D; }
 template <int R>
 struct Ops64 {
     double2 a[2];
@@ -376,8 +362,6 @@ struct RowMap {
     int bi[MAXR];
     int nown;
 };
-constexpr int kBalTab[7][3] = {{2, 10, 99}, {3, 11, 99}, {0, 1, 8}, {5, 9, 12}, {4, 13, 99}, {7, 14, 99}, {6, 15, 99}};
-constexpr int kBalCnt[7] = {2, 2, 3, 3, 2, 2, 2};
 template <int MAXR, int NA>
 __device__ __forceinline__ RowMap<MAXR> row_map(int wr, int nt) {
     RowMap<MAXR> m;
@@ -387,112 +371,23 @@ __device__ __forceinline__ RowMap<MAXR> row_map(int wr, int nt) {
     m.nown = wr < nt ? (nt - wr + NA - 1) / NA : 0;
     if constexpr (RVK_GP64_BAL && RVK_GP64_RING > 1 && MAXR == 3 && NA == 7) {
         if (nt == 16) {
+            constexpr int tab[7][3] = {{2, 10, 99}, {3, 11, 99}, {0, 1, 8}, {5, 9, 12}, {4, 13, 99}, {7, 14, 99}, {6, 15, 99}};
+            constexpr int cnt[7] = {2, 2, 3, 3, 2, 2, 2};
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 int v = 99;
 #pragma unroll
-                for (int w = 0; w < 7; ++w) v = wr == w ? kBalTab[w][q] : v;
+                for (int w = 0; w < 7; ++w) v = wr == w ? tab[w][q] : v;
                 m.bi[q] = v;
             }
             int c = 0;
 #pragma unroll
-            for (int w = 0; w < 7; ++w) c = wr == w ? kBalCnt[w] : c;
+            for (int w = 0; w < 7; ++w) c = wr == w ? cnt[w] : c;
             m.nown = c;
         }
     }
     return m;
 }
-
-// RVK_GP64_HELP (the LDS-slot shape: nt <= 16, 7 row waves + the factor wave): the accumulation of a
-// step is split over the SIMDs, not only over the owned rows.  A step's accumulation ends at a barrier,
-// so the step lasts as long as its busiest SIMD's matrix pipe (waves w and w + 4 share SIMD w mod 4);
-// with whole rows per wave that SIMD carries up to 2 rows where the others carry 1 or none (the
-// tail: at k = 13 two SIMDs work, at k = 14 one), 204 row products on the busiest SIMDs over the 16
-// steps of n = 512 against 140 if even.  So a wave may hand the END of its rows' j-range, quarters
-// [lo, hi) of all its live rows (their A operand loads stay shared), to a helper wave on a less loaded
-// SIMD; the helper accumulates those quarters into zeroed registers before its own rows and parks the
-// partial sums in LDS slots that are free during the step (the slots of the finished rows 1 .. k:
-// pslot(bi) is last read by S2(bi - 1)); the owner adds them to its accumulators in S2, after B2.  The
-// split depends only on (nt, k): a compile-time table, computed by the greedy below (largest SIMD load
-// hands to the smallest, one piece per helper, until within two quarters of a row).
-#ifndef RVK_GP64_HELP
-#define RVK_GP64_HELP 0   // measured slower (profiles/round6/gp64/ab_help_ring.json)
-#endif
-struct HelpEnt {
-    signed char own;     // quarters [0, own) of this wave's live rows it accumulates itself
-    signed char donor;   // -1, or the wave whose rows this wave helps with
-    signed char lo, hi;  // the donor's quarters [lo, hi) this wave accumulates
-    signed char slot;    // first LDS slot index of the partials (one per donor live row, in row order)
-    signed char ps[3];   // as a donor: the first slot of each piece handed out (-1: none)
-};
-#ifndef RVK_GP64_HELP_S3
-#define RVK_GP64_HELP_S3 0   // 1: SIMD 3 (the factor wave's) may receive pieces too
-#endif
-struct HelpTab {
-    HelpEnt e[17][16][8];   // [nt][k][wave]
-};
-constexpr int help_row(int w, int q, int nt) {   // row_map<3, 7>'s rows (99: none)
-    if (RVK_GP64_BAL && RVK_GP64_RING > 1 && nt == 16) return q < kBalCnt[w] ? kBalTab[w][q] : 99;
-    const int bi = w + 7 * q;
-    return bi < nt ? bi : 99;
-}
-constexpr HelpTab make_help_tab() {
-    HelpTab t{};
-    for (int nt = 0; nt <= 16; ++nt)
-        for (int k = 0; k < 16; ++k) {
-            for (int w = 0; w < 8; ++w) t.e[nt][k][w] = HelpEnt{(signed char)(4 * k), -1, 0, 0, 0, {-1, -1, -1}};
-            if (k == 0 || k + 1 >= nt) continue;             // no products (k = 0) / no next column
-            int R[7] = {}, wt[7] = {}, own[7] = {}, load[7] = {}, S[4] = {}, npc[7] = {};
-            bool helped[7] = {};
-            for (int w = 0; w < 7; ++w) {
-                for (int q = 0; q < 3; ++q) {
-                    const int bi = help_row(w, q, nt);
-                    if (bi >= k + 1 && bi < nt) {
-                        R[w] += 1;
-                        wt[w] += bi == k + 1 ? 6 : 8;        // MFMAs per quarter (HALFDIAG diagonal row: 6)
-                    }
-                }
-                own[w] = 4 * k;
-                load[w] = own[w] * wt[w];
-                S[w & 3] += load[w];
-            }
-            int nslot = 0;
-            for (int it = 0; it < 8; ++it) {
-                const int tot = S[0] + S[1] + S[2] + S[3], T = (tot + 3) / 4;
-                int smax = 0, smin = 0;
-                for (int s = 1; s < 4; ++s) {
-                    if (S[s] > S[smax]) smax = s;
-                    if ((RVK_GP64_HELP_S3 || s < 3) && S[s] < S[smin]) smin = s;
-                }
-                if (S[smax] - S[smin] < 16) break;            // within two quarters of a row
-                int d = -1, h = -1;
-                for (int w = 0; w < 7; ++w)
-                    if ((w & 3) == smax && wt[w] > 0 && own[w] > 0 && npc[w] < 3 && (d < 0 || load[w] > load[d])) d = w;
-                for (int w = 0; w < 7; ++w)
-                    if ((w & 3) == smin && !helped[w] && (h < 0 || load[w] < load[h])) h = w;
-                if (d < 0 || h < 0) break;
-                const int mv = (S[smax] - T) < (T - S[smin]) ? (S[smax] - T) : (T - S[smin]);
-                int x = (mv + wt[d] / 2) / wt[d];
-                if (x > own[d]) x = own[d];
-                if (x <= 0 || nslot + R[d] > k) break;
-                t.e[nt][k][h].donor = (signed char)d;
-                t.e[nt][k][h].lo = (signed char)(own[d] - x);
-                t.e[nt][k][h].hi = (signed char)own[d];
-                t.e[nt][k][h].slot = (signed char)nslot;
-                t.e[nt][k][d].ps[npc[d]++] = (signed char)nslot;
-                nslot += R[d];
-                own[d] -= x;
-                helped[h] = true;
-                load[d] -= x * wt[d];
-                load[h] += x * wt[d];
-                S[smax] -= x * wt[d];
-                S[smin] += x * wt[d];
-            }
-            for (int w = 0; w < 7; ++w) t.e[nt][k][w].own = (signed char)own[w];
-        }
-    return t;
-}
-__constant__ constexpr HelpTab kHelpTab = make_help_tab();
 
 // HALFDIAG: a diagonal tile's block above the diagonal (rows 0-15, columns 16-31: C/D block
 // c[1][0]) is never formed -- no covariance, no accumulation MFMAs, no S2 MFMAs: the
@@ -513,20 +408,17 @@ __constant__ constexpr HelpTab kHelpTab = make_help_tab();
 #endif
 template <int MAXR, int NA, int A, int B, int D>
 __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, const RowMap<MAXR> &rm,
-                                           int lane, int h0, int h1) {
+                                           int lane) {
     constexpr int R = B - A + 1;
     const bool dg = RVK_GP64_HALFDIAG && rm.bi[A] == k + 1;   // wave-uniform
-    // quarters (j, part) h0 <= 4 j + part < h1, j < k (the LDS-slot shape; the 5-row kernels keep
-    // [0, 4 k) in their own code, so their register allocation stays the one measured)
-    const int NQ = MAXR == 3 ? h1 - h0 : 4 * k;
-    h0 = MAXR == 3 ? h0 : 0;
+    const int NQ = 4 * k;                           // quarters (j, part), j < k
     const double2 *rowa = reinterpret_cast<const double2 *>(wk + tix(k + 1, 0) * TILE) + lane;
     const double2 *rowb[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) rowb[r] = reinterpret_cast<const double2 *>(wk + tix(rm.bi[A + r], 0) * TILE) + lane;
     Ops64<R> ops[D];
     auto issue = [&](Ops64<R> &o, int hx) {         // unconditional (clamped past the end): the
-        hx = h0 + (hx < NQ ? hx : NQ - 1);          // wait counts stay exact on every path
+        hx = hx < NQ ? hx : NQ - 1;                 // wait counts stay exact on every path
         const int j = hx >> 2, part = hx & 3;
         const int off = j * (TILE / 2) + part * 64;  // double2 units: tiles of row bi are contiguous in j
         const int offa = (RVK_GP64_ABLATE & 1) ? part * 64 : off, offb = (RVK_GP64_ABLATE & 2) ? part * 64 : off;
@@ -568,13 +460,12 @@ __device__ __forceinline__ void accum_span(Acc (&acc)[MAXR], const double *__res
 // The live rows A0 .. B0 of a wave (a suffix of its rows: rows finish in order), in spans of <= 3.
 template <int MAXR, int NA, int D>
 __device__ __forceinline__ void accum_rows(Acc (&acc)[MAXR], const double *__restrict__ wk, int k, const RowMap<MAXR> &rm,
-                                           int lane, int a0, int b0, int h0, int h1) {
-    if (MAXR == 3 && h1 <= h0) return;
+                                           int lane, int a0, int b0) {
     for (int a = a0; a <= b0; a += 3) {
         const int b = a + 2 < b0 ? a + 2 : b0;
 #define RVK_SPAN(X, Y)                                                                   \
     if constexpr (Y < MAXR) {                                                            \
-        if (a == X && b == Y) accum_span<MAXR, NA, X, Y, ring_for<MAXR, Y - X + 1, D>()>(acc, wk, k, rm, lane, h0, h1); \
+        if (a == X && b == Y) accum_span<MAXR, NA, X, Y, D>(acc, wk, k, rm, lane);       \
     }
         RVK_SPAN(0, 0) RVK_SPAN(0, 1) RVK_SPAN(0, 2) RVK_SPAN(1, 1) RVK_SPAN(1, 2) RVK_SPAN(1, 3)
         RVK_SPAN(2, 2) RVK_SPAN(2, 3) RVK_SPAN(2, 4) RVK_SPAN(3, 3) RVK_SPAN(3, 4) RVK_SPAN(4, 4)
@@ -600,7 +491,6 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
     // accumulator acc(bi, k) (S2(k-1) -> S1(k)) and its new factor tile L(bi, k) (S1(k) -> S2(k)),
     // so S1 and S2 read their operands from LDS instead of the workspace (15 x 8 KB at n = 512)
     constexpr bool LDSP = gp64_ldsp<MAXR, GROUPED>();
-    constexpr bool HELP = RVK_GP64_HELP && LDSP && RVK_GP64_RING > 1 && NW == 8;   // kHelpTab's shape
     double *slots = smem64;           // [nt - 1][TILE] (LDSP)
     auto pslot = [&](int bi) { return (lds_d *)(slots + (bi - 1) * TILE); };
     double *Lt = smem64 + (LDSP ? (nt - 1) * TILE : 0);   // [npad] epochs (padding: t[n-1])
@@ -813,30 +703,6 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
 #pragma unroll
                             for (int qq = 0; qq < 2; ++qq) nacc[q].c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
                 }
-                int own_hi = 4 * k;                         // quarters of the own rows this wave accumulates
-                if constexpr (HELP) {
-                    if (k > 0 && k + 1 < nt) {
-                        const HelpEnt he = kHelpTab.e[nt][k][wr];
-                        own_hi = he.own;
-                        if (he.donor >= 0) {                // the donor's quarters [lo, hi): partials to LDS
-                            const RowMap<MAXR> rd = row_map<MAXR, NA>(he.donor, nt);
-                            int d0 = rd.nown;
-#pragma unroll
-                            for (int q = MAXR - 1; q >= 0; --q)
-                                if (q < rd.nown && rd.bi[q] >= k + 1) d0 = q;
-                            accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, rd, lane, d0, rd.nown - 1, he.lo, he.hi);
-#pragma unroll
-                            for (int q = 0; q < MAXR; ++q)
-                                if (q >= d0 && q < rd.nown) {
-                                    park(pslot(1 + he.slot + q - d0), nacc[q], lane);
-#pragma unroll
-                                    for (int p = 0; p < 2; ++p)
-#pragma unroll
-                                        for (int qq = 0; qq < 2; ++qq) nacc[q].c[p][qq] = f64x4{0.0, 0.0, 0.0, 0.0};
-                                }
-                        }
-                    }
-                }
                 for (int qo = 0; qo < (grouped ? nown : 1) && k + 1 < nt; qo += MAXR) {   // one trip unless grouped
                     if (grouped && wr + NA * (qo + MAXR - 1) < k + 1) continue;    // the group's rows are finished
 #pragma unroll
@@ -915,7 +781,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         for (int q = MAXR - 1; q >= 0; --q)
                             if (q < nown && rm.bi[q] >= k + 1) r0 = q;
                         if (k > 0 && r0 < nown && !(RVK_GP64_ABLATE & 8))
-                            accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, rm, lane, r0, nown - 1, 0, own_hi);
+                            accum_rows<MAXR, NA, RVK_GP64_RING>(nacc, wk, k, rm, lane, r0, nown - 1);
                     } else {
                         pass(std::integral_constant<int, 0>{});
                         if constexpr (MAXR > 2) pass(std::integral_constant<int, 2>{});
@@ -1050,21 +916,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                 if constexpr (LDSP && RVK_GP64_S1HALF) load_slot_frags(pslot(k + 1), af, lane);
                 else if constexpr (LDSP) load_frags(pslot(k + 1), af, lane);
                 else load_frags(wk + tix(k + 1, k) * TILE, af, lane);
-                HelpEnt me{};
-                if constexpr (HELP) me = kHelpTab.e[nt][k][wr];
-                auto s2 = [&](Acc &acc, int bi, int qoff) {
-                    if constexpr (HELP) {                   // the helpers' partial sums of this row
-#pragma unroll
-                        for (int i = 0; i < 3; ++i)
-                            if (me.ps[i] >= 0) {
-                                Acc pa;
-                                unpark(pslot(1 + me.ps[i] + qoff), pa, lane);
-#pragma unroll
-                                for (int p = 0; p < 2; ++p)
-#pragma unroll
-                                    for (int qq = 0; qq < 2; ++qq) acc.c[p][qq] += pa.c[p][qq];
-                            }
-                    }
+                auto s2 = [&](Acc &acc, int bi) {
                     double bf[2][8];
                     if constexpr (LDSP && RVK_GP64_S1HALF) load_slot_frags(pslot(bi), bf, lane);
                     else if constexpr (LDSP) load_frags(pslot(bi), bf, lane);
@@ -1083,14 +935,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                     else park(wk + tix(bi, k + 1) * TILE, acc, lane);
                 };
                 if constexpr (!grouped) {
-                    int r0 = nown;                              // the first live row (partials by row order)
-#pragma unroll
-                    for (int q = MAXR - 1; q >= 0; --q)
-                        if (q < nown && rm.bi[q] > k) r0 = q;
 #pragma unroll
                     for (int q = 0; q < MAXR; ++q) {
                         const int bi = rm.bi[q];
-                        if (bi > k && bi < nt && q < nown) s2(nacc[q], bi, q - r0);
+                        if (bi > k && bi < nt && q < nown) s2(nacc[q], bi);
                     }
                 } else {
                     for (int q = 0; q < nown; ++q) {
@@ -1098,7 +946,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
                         if (bi > k && bi < nt) {
                             Acc acc;
                             unpark(wk + tix(bi, k + 1) * TILE, acc, lane);
-                            s2(acc, bi, 0);
+                            s2(acc, bi);
                         }
                     }
                 }
