@@ -479,7 +479,7 @@ __device__ __forceinline__ void accum_rows(Acc (&acc)[MAXR], const double *__res
 template <int MAXR, bool GROUPED>
 constexpr bool gp64_ldsp() { return RVK_GP64_LDSPARK && MAXR == 3 && !GROUPED; }
 
-// MAXR tile rows per row-owning wave; GROUPED: nt > MAXR * (NW - 1), the rows go through the workspace in
+// MAXR tile rows per row-owning wave; GROUPED: the rows go through the workspace in
 // groups of MAXR (a separate instantiation: the common shape keeps its register allocation)
 template <int NW, int MAXR, bool COND, bool GROUPED>
 __global__ __launch_bounds__(64 * NW, 1) void gp64_kernel(const Gp64Args a) {
@@ -1033,14 +1033,22 @@ namespace rvk {
 
 Gp64Shape gp64_shape(int n) {
     const int nt = (n + TB - 1) / TB;
-    // 7 row-owning waves + the factor wave; beyond 7 x 5 tile rows the rows are grouped
-    return nt <= 16 ? Gp64Shape{8, 3, false} : nt <= 35 ? Gp64Shape{8, 5, false} : Gp64Shape{8, 5, true};
+    // 7 row-owning waves + the factor wave.  nt <= 16: three accumulator rows per wave, parked in LDS
+    // slots; 17..35: the rows go through the workspace in groups of three; beyond: groups of five.
+    // (Round 6, fp64, 4096 walkers: the grouped 3-row kernel -- 0 VGPRs spilled, 96 B of scratch --
+    // against the ungrouped 5-row kernel it replaces for 17..35 -- 253 VGPRs spilled, 944 B --
+    // n = 700 16.6 vs 20.4 ms, n = 1024 48.2 vs 52.1; at n = 2048 the 5-row groups stay ahead, 373.9
+    // vs 377.9; at n = 512 the LDS-slot kernel stays ahead of any grouped form, 5.65 vs 7.2 ms;
+    // profiles/round6/gp64/ab_shapes.json.  The ungrouped 5-row kernel was also the one whose
+    // register allocation faulted twice at n = 700 under semantically neutral changes: DESIGN §3.)
+    return nt <= 16 ? Gp64Shape{8, 3, false} : nt <= 35 ? Gp64Shape{8, 3, true} : Gp64Shape{8, 5, true};
 }
 
 size_t gp64_lds_bytes(int n, int np, int nw) {
     const int nt = (n + TB - 1) / TB;
     size_t b = sizeof(double) * ((RVK_GP64_SINADD ? 4 : 3) * (size_t)nt * TB + TB * FS + TILE + 2 * (size_t)nw);
-    if (gp64_shape(n).maxr == 3 && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
+    const Gp64Shape sh = gp64_shape(n);
+    if (sh.maxr == 3 && !sh.grouped && gp64_ldsp<3, false>()) b += sizeof(double) * (size_t)(nt - 1) * TILE;   // LDS slots
     b += sizeof(SC) * kTabN + (sizeof(PlanetK) + sizeof(int)) * (size_t)np + 16;
     return b;
 }
@@ -1054,8 +1062,8 @@ gp64_launch_t pick_gp64(int np, bool multi, bool tp, bool condition, Gp64Shape s
     (void)multi;
     (void)tp;
     if (np < 1 || np > RVK_MAX_PLANETS) return nullptr;
-    if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true, false> : launch_gp64<8, 3, false, false>;
-    if (!sh.grouped) return condition ? launch_gp64<8, 5, true, false> : launch_gp64<8, 5, false, false>;
+    if (sh.maxr == 3 && !sh.grouped) return condition ? launch_gp64<8, 3, true, false> : launch_gp64<8, 3, false, false>;
+    if (sh.maxr == 3) return condition ? launch_gp64<8, 3, true, true> : launch_gp64<8, 3, false, true>;
     return condition ? launch_gp64<8, 5, true, true> : launch_gp64<8, 5, false, true>;
 }
 
