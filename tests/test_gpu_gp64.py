@@ -65,7 +65,11 @@ def _walkers(ds, W, seed, **kw):
                                                 (1, 1, 1, "P K e w Tp", False),
                                                 (700, 1, 1, "P K e w Tp", False),
                                                 (1024, 2, 2, "P K secosw sesinw Tc", True),
-                                                (150, 10, 12, "P K e w Tc", True)])   # > 8 planets
+                                                (150, 10, 12, "P K e w Tc", True),   # > 8 planets
+                                                # the kernel-shape edges (rvk_gp64.hip gp64_shape): 16 tile rows
+                                                # with LDS slots | 17-35 in groups of three | 36+ in groups of five
+                                                (513, 1, 1, "P K e w Tp", False), (1120, 1, 2, "P K e w Tc", True),
+                                                (1121, 1, 1, "P K e w Tp", False)])
 def test_fp64_loglike_vs_oracle(n, np_, ni, par, trend):
     from ravest_amd.synth import make_dataset
     ds = make_dataset(np_, n, ni, seed=150 + n, parameterisation=par, trend=trend)
@@ -173,7 +177,8 @@ def test_not_positive_definite_in_fp64_is_nan():
 # ---- GP-conditioned posterior predictive -----------------------------------------------------
 
 @pytest.mark.parametrize("n,np_,ni,par,T", [(120, 1, 1, "P K e w Tp", 300), (200, 2, 2, "P K secosw sesinw Tc", 97),
-                                             (33, 1, 1, "P K e w Tc", 1), (520, 1, 1, "P K e w Tp", 64)])
+                                             (33, 1, 1, "P K e w Tc", 1), (520, 1, 1, "P K e w Tp", 64),
+                                             (1120, 1, 1, "P K e w Tp", 33)])
 def test_gp_condition_vs_oracle(n, np_, ni, par, T):
     from oracle import gp_oracle
     from ravest_amd.synth import make_dataset
