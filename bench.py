@@ -805,18 +805,28 @@ def grouped_steps(args, eng, th_d, W: int, world: int, backend: str, dev) -> dic
 
     graph = None
     if mode in ("graph", "none"):
+        ok, err = 1, ""
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
                 issue_all(cap)
+        except Exception as e:                        # capture of the collective refused on this rank
+            ok, err, graph = 0, str(e), None
+        torch.cuda.synchronize(dev)
+        # The choice must be the same on every rank: a rank that replays a graph holding the
+        # all-gather while another took the host-issued form would wait in that gather for a
+        # peer that never joins it.  Capture runs nothing, so no collective has run yet.
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 1:
             graph.replay()                            # warm replay
             torch.cuda.synchronize(dev)
             region = graph.replay
-        except Exception as e:                        # capture of the collective refused: host-issued form
-            print(f"bench.py: HIP-graph capture of the all-gather failed ({e}); using --gather stream",
+        else:                                         # host-issued form on every rank
+            why = err or "on another rank"
+            print(f"bench.py: HIP-graph capture of the all-gather failed ({why}); using --gather stream",
                   file=sys.stderr, flush=True)
             graph, mode = None, "stream"
-            torch.cuda.synchronize(dev)
     if graph is None:
         gg = []
         for r in range(R):                            # G-launch kernel graphs, one per output buffer
