@@ -1008,7 +1008,7 @@ def main():
             line["gp_config5"] = gp_line()
         if world == 1 and not args.no_predictive:
             line["predictive"] = predictive_line(eng, theta)
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:     # rank 0 at N = 1 only (the other ranks would wait)
             line["cpu_baseline"] = cpu_baseline(ds, theta, args.cpu_seconds)
     if not args.no_configs:
         c4 = config4_sharded_line(world, rank, backend, grouped)   # collective: every rank takes part
