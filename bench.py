@@ -807,6 +807,8 @@ def grouped_steps(args, eng, th_d, W: int, world: int, backend: str, dev) -> dic
     if mode in ("graph", "none"):
         ok, err = 1, ""
         try:
+            if os.environ.get("RVK_BENCH_NO_CAPTURE") == os.environ.get("RANK", "0"):   # exercises the fallback
+                raise RuntimeError("capture refused on this rank by RVK_BENCH_NO_CAPTURE")
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
                 issue_all(cap)
